@@ -1,0 +1,824 @@
+// golhip_engine.hip -- host side of libgolhip: handles, device memory, streams, RCCL halo
+// exchange and the C ABI declared in include/golhip.h.
+//
+// Reference roles this file takes over (Oliver-Cairns/distributed-gol):
+//   * broker/broker.go:37-56  publish(): split the rows into strips -> golhip_strip_bounds(),
+//     one strip per GPU (the reference's 4 servers become the node's GPUs);
+//   * broker/broker.go:58-84,157-180  subscriberLoop/Publish: fan the FULL world out every turn
+//     and stitch the strips back -> the board stays resident in HBM, only k halo rows per strip
+//     edge move per k generations, by RCCL send/recv over xGMI on a dedicated comm stream that
+//     overlaps the interior update;
+//   * broker/broker.go:124-155  CheckStates/Pause (worldSave, turn) -> the resident board and
+//     golhip_turn()/golhip_set_turn().
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/golhip.h"
+#include "golhip_internal.hpp"
+
+using golhip::StencilParams;
+
+namespace {
+
+constexpr int kVersion = 100;
+
+struct Shard {
+    int device = 0;
+    int rank = 0;
+    int64_t y0 = 0, rows = 0;
+    hipStream_t compute = nullptr, comm = nullptr;
+    hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
+    uint32_t *buf[2] = {nullptr, nullptr};  // allocation base (halo rows first)
+    unsigned long long *slots = nullptr;    // kMaxK * kCountSlots
+    unsigned long long *scratch_u64 = nullptr;
+    unsigned long long *d_counts = nullptr;
+    size_t d_counts_cap = 0;
+    ncclComm_t comm_nccl = nullptr;
+};
+
+struct TimingPair {
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct golhip_engine {
+    int64_t width = 0, height = 0, L = 0, pitch = 0;
+    int32_t wd = 0;
+    int world_size = 1;
+    int k = 1, halo = 0, band_rows = 0;
+    bool rank_mode = false;
+    std::vector<Shard> shards;
+    int cur = 0;
+    bool prev_valid = false;
+    int64_t turn = 0;
+    std::string err;
+    // timing
+    bool timing = false;
+    std::vector<TimingPair> tpool;
+    size_t tused = 0;
+    double tms = 0.0;
+    int64_t tlaunches = 0, tgens = 0;
+
+    uint32_t *row0(const Shard &s, int which) const {
+        return s.buf[which] + (int64_t)halo * pitch;
+    }
+    int64_t rep() const { return L / width; }
+};
+
+namespace {
+
+int fail(golhip_t h, int code, const char *fmt, ...) {
+    if (h) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        h->err = buf;
+    }
+    return code;
+}
+
+#define HIPCHK(h, expr)                                                                     \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return fail((h), e_ == hipErrorOutOfMemory ? GOLHIP_ERR_OOM : GOLHIP_ERR_HIP,   \
+                        "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+    } while (0)
+
+#define NCCLCHK(h, expr)                                                                    \
+    do {                                                                                    \
+        ncclResult_t r_ = (expr);                                                           \
+        if (r_ != ncclSuccess)                                                              \
+            return fail((h), GOLHIP_ERR_RCCL, "%s: %s (%s:%d)", #expr,                      \
+                        ncclGetErrorString(r_), __FILE__, __LINE__);                        \
+    } while (0)
+
+int64_t lcm64(int64_t a, int64_t b) { return a / std::gcd(a, b) * b; }
+
+void strip_bounds(int64_t height, int world, int rank, int64_t &y0, int64_t &rows) {
+    // balanced contiguous split (the reference's publish() splits ImageSize/numServers and hands
+    // the remainder to the first strips, broker/broker.go:38-46; same coverage here, any height)
+    y0 = height * rank / world;
+    rows = height * (rank + 1) / world - y0;
+}
+
+int check_device_arch(golhip_t h, int device) {
+    hipDeviceProp_t prop;
+    HIPCHK(h, hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(h, GOLHIP_ERR_NODEV, "device %d is %s, libgolhip is built for gfx950", device,
+                    prop.gcnArchName);
+    return GOLHIP_OK;
+}
+
+int alloc_shard(golhip_t h, Shard &s) {
+    HIPCHK(h, hipSetDevice(s.device));
+    HIPCHK(h, hipStreamCreateWithFlags(&s.compute, hipStreamNonBlocking));
+    HIPCHK(h, hipStreamCreateWithFlags(&s.comm, hipStreamNonBlocking));
+    HIPCHK(h, hipEventCreateWithFlags(&s.ev_ready, hipEventDisableTiming));
+    HIPCHK(h, hipEventCreateWithFlags(&s.ev_halo, hipEventDisableTiming));
+    const size_t words = (size_t)(s.rows + 2 * (int64_t)h->halo) * (size_t)h->pitch;
+    for (int i = 0; i < 2; ++i) {
+        HIPCHK(h, hipMalloc(&s.buf[i], words * sizeof(uint32_t)));
+        HIPCHK(h, hipMemsetAsync(s.buf[i], 0, words * sizeof(uint32_t), s.compute));
+    }
+    HIPCHK(h, hipMalloc(&s.slots, sizeof(unsigned long long) * golhip::kMaxK * golhip::kCountSlots));
+    HIPCHK(h, hipMemsetAsync(s.slots, 0,
+                             sizeof(unsigned long long) * golhip::kMaxK * golhip::kCountSlots,
+                             s.compute));
+    HIPCHK(h, hipMalloc(&s.scratch_u64, sizeof(unsigned long long) * 4));
+    HIPCHK(h, hipStreamSynchronize(s.compute));
+    return GOLHIP_OK;
+}
+
+void free_shard(Shard &s) {
+    (void)hipSetDevice(s.device);
+    if (s.compute) (void)hipStreamSynchronize(s.compute);
+    if (s.comm) (void)hipStreamSynchronize(s.comm);
+    if (s.comm_nccl) (void)ncclCommDestroy(s.comm_nccl);
+    for (auto &b : s.buf)
+        if (b) (void)hipFree(b);
+    if (s.slots) (void)hipFree(s.slots);
+    if (s.scratch_u64) (void)hipFree(s.scratch_u64);
+    if (s.d_counts) (void)hipFree(s.d_counts);
+    if (s.ev_ready) (void)hipEventDestroy(s.ev_ready);
+    if (s.ev_halo) (void)hipEventDestroy(s.ev_halo);
+    if (s.compute) (void)hipStreamDestroy(s.compute);
+    if (s.comm) (void)hipStreamDestroy(s.comm);
+    s = Shard{};
+}
+
+int validate_geometry(int width, int height, int world, int k) {
+    if (width <= 0 || height <= 0 || world <= 0) return GOLHIP_ERR_ARG;
+    if (k < 1 || k > golhip::kMaxK) return GOLHIP_ERR_ARG;
+    // row strips must be able to send k halo rows to each neighbour (a single strip wraps
+    // rows modulo the height and needs nothing)
+    if (world > 1 && (int64_t)height / world < k) return GOLHIP_ERR_ARG;
+    return GOLHIP_OK;
+}
+
+int setup_engine(golhip_t h, int width, int height, int world, int k) {
+    h->width = width;
+    h->height = height;
+    h->L = lcm64(width, 128);
+    h->wd = (int32_t)(h->L / 32);
+    h->pitch = h->wd;
+    h->world_size = world;
+    h->k = k;
+    h->halo = world > 1 ? k : 0;
+    if (const char *e = std::getenv("GOLHIP_BAND_ROWS")) h->band_rows = std::atoi(e);
+    return GOLHIP_OK;
+}
+
+// Largest supported launch depth <= n.
+int pick_k(int n) {
+    int kk = 1;
+    for (int c : {32, 16, 8, 4, 2, 1})
+        if (c <= n && golhip::stencil_k_supported(c)) {
+            kk = c;
+            break;
+        }
+    return kk;
+}
+
+int64_t auto_band(golhip_t h, int64_t rows_total, int K) {
+    if (h->band_rows > 0) return h->band_rows;
+    const int64_t nchunks = (h->wd + 61) / 62;
+    // aim for ~4096 waves in flight (16 per CU), bands at least 4K rows tall so the 2K-row
+    // pipeline fill stays small, at most 1024 rows
+    int64_t target_bands = std::max<int64_t>(1, 4096 / nchunks);
+    int64_t band = (rows_total + target_bands - 1) / target_bands;
+    band = std::max<int64_t>(band, std::min<int64_t>(4 * K, rows_total));
+    band = std::max<int64_t>(band, 4);
+    band = std::min<int64_t>(band, 1024);
+    return band;
+}
+
+StencilParams make_params(golhip_t h, const Shard &s, int K, int64_t r0b, int64_t r0e,
+                          int64_t r1b, int64_t r1e) {
+    StencilParams p{};
+    p.pitch = h->pitch;
+    p.r0b = r0b;
+    p.r0e = r0e;
+    p.r1b = r1b;
+    p.r1e = r1e;
+    const int64_t total = (r0e - r0b) + (r1e - r1b);
+    p.band = auto_band(h, std::max<int64_t>(total, 1), K);
+    p.nbands0 = (r0e - r0b + p.band - 1) / p.band;
+    p.nbands = p.nbands0 + (r1e - r1b + p.band - 1) / p.band;
+    p.wrap_rows = h->world_size == 1 ? h->height : 0;
+    p.lo = -(int64_t)h->halo;
+    p.hi = s.rows + h->halo;
+    p.wd = h->wd;
+    p.nchunks = (h->wd + 61) / 62;
+    return p;
+}
+
+int timing_begin(golhip_t h, Shard &s, hipEvent_t *stop) {
+    *stop = nullptr;
+    if (!h->timing || &s != &h->shards[0]) return GOLHIP_OK;
+    if (h->tused == h->tpool.size()) {
+        TimingPair tp;
+        HIPCHK(h, hipEventCreate(&tp.a));
+        HIPCHK(h, hipEventCreate(&tp.b));
+        h->tpool.push_back(tp);
+    }
+    TimingPair &tp = h->tpool[h->tused++];
+    HIPCHK(h, hipEventRecord(tp.a, s.compute));
+    *stop = tp.b;
+    return GOLHIP_OK;
+}
+
+int timing_collect(golhip_t h) {
+    if (h->tused == 0) return GOLHIP_OK;
+    HIPCHK(h, hipSetDevice(h->shards[0].device));
+    for (size_t i = 0; i < h->tused; ++i) {
+        HIPCHK(h, hipEventSynchronize(h->tpool[i].b));
+        float ms = 0.f;
+        HIPCHK(h, hipEventElapsedTime(&ms, h->tpool[i].a, h->tpool[i].b));
+        h->tms += ms;
+    }
+    h->tused = 0;
+    return GOLHIP_OK;
+}
+
+// Exchange K halo rows between neighbouring strips (toroidal ring) on the comm streams.
+int exchange_halos(golhip_t h, int K) {
+    const int W = h->world_size;
+    const size_t bytes = (size_t)K * (size_t)h->pitch * sizeof(uint32_t);
+    for (auto &s : h->shards) {
+        HIPCHK(h, hipSetDevice(s.device));
+        HIPCHK(h, hipEventRecord(s.ev_ready, s.compute));
+        HIPCHK(h, hipStreamWaitEvent(s.comm, s.ev_ready, 0));
+    }
+    NCCLCHK(h, ncclGroupStart());
+    for (auto &s : h->shards) {
+        const int up = (s.rank - 1 + W) % W, down = (s.rank + 1) % W;
+        uint32_t *r0 = h->row0(s, h->cur);
+        // Order matters when up == down (W == 2): sends to `down` first, receives from `up`
+        // first, so the i-th send of one rank matches the i-th receive of its peer.
+        NCCLCHK(h, ncclSend(r0 + (s.rows - K) * h->pitch, bytes, ncclUint8, down, s.comm_nccl,
+                            s.comm));
+        NCCLCHK(h, ncclSend(r0, bytes, ncclUint8, up, s.comm_nccl, s.comm));
+        NCCLCHK(h, ncclRecv(r0 - (int64_t)K * h->pitch, bytes, ncclUint8, up, s.comm_nccl,
+                            s.comm));
+        NCCLCHK(h, ncclRecv(r0 + s.rows * h->pitch, bytes, ncclUint8, down, s.comm_nccl,
+                            s.comm));
+    }
+    NCCLCHK(h, ncclGroupEnd());
+    for (auto &s : h->shards) {
+        HIPCHK(h, hipSetDevice(s.device));
+        HIPCHK(h, hipEventRecord(s.ev_halo, s.comm));
+    }
+    return GOLHIP_OK;
+}
+
+// One K-generation block on every shard. counts_dev_off: index into s.d_counts (or -1).
+int step_block(golhip_t h, int K, int64_t counts_off) {
+    if (h->world_size > 1) {
+        int rc = exchange_halos(h, K);
+        if (rc) return rc;
+    }
+    const int nxt = h->cur ^ 1;
+    for (auto &s : h->shards) {
+        HIPCHK(h, hipSetDevice(s.device));
+        unsigned long long *slots = counts_off >= 0 ? s.slots : nullptr;
+        const uint32_t *in = h->row0(s, h->cur);
+        uint32_t *out = h->row0(s, nxt);
+        hipEvent_t stop = nullptr;
+        int rc = timing_begin(h, s, &stop);
+        if (rc) return rc;
+        if (h->world_size == 1) {
+            StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0);
+            HIPCHK(h, golhip::launch_stencil(K, in, out, p, slots, s.compute));
+        } else if (s.rows >= 3 * K) {
+            // interior rows need no halo: overlap them with the exchange
+            StencilParams pi = make_params(h, s, K, K, s.rows - K, 0, 0);
+            HIPCHK(h, golhip::launch_stencil(K, in, out, pi, slots, s.compute));
+            HIPCHK(h, hipStreamWaitEvent(s.compute, s.ev_halo, 0));
+            StencilParams pb = make_params(h, s, K, 0, K, s.rows - K, s.rows);
+            HIPCHK(h, golhip::launch_stencil(K, in, out, pb, slots, s.compute));
+        } else {
+            HIPCHK(h, hipStreamWaitEvent(s.compute, s.ev_halo, 0));
+            StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0);
+            HIPCHK(h, golhip::launch_stencil(K, in, out, p, slots, s.compute));
+        }
+        if (stop) HIPCHK(h, hipEventRecord(stop, s.compute));
+        if (counts_off >= 0)
+            HIPCHK(h, golhip::launch_count_finalize(K, s.slots, s.d_counts + counts_off,
+                                                     s.compute));
+    }
+    if (h->timing) {
+        h->tlaunches += 1;
+        h->tgens += K;
+        if (h->tused >= 1024) {
+            int rc = timing_collect(h);
+            if (rc) return rc;
+        }
+    }
+    h->cur = nxt;
+    h->turn += K;
+    h->prev_valid = (K == 1);
+    return GOLHIP_OK;
+}
+
+int sync_all(golhip_t h) {
+    for (auto &s : h->shards) {
+        HIPCHK(h, hipSetDevice(s.device));
+        HIPCHK(h, hipStreamSynchronize(s.comm));
+        HIPCHK(h, hipStreamSynchronize(s.compute));
+    }
+    return GOLHIP_OK;
+}
+
+// Sum n uint64 values (device, per shard) over every rank; result in shard 0's buffer.
+int allreduce_u64(golhip_t h, std::vector<unsigned long long *> bufs, size_t n) {
+    if (h->world_size == 1) return GOLHIP_OK;
+    NCCLCHK(h, ncclGroupStart());
+    for (size_t i = 0; i < h->shards.size(); ++i) {
+        Shard &s = h->shards[i];
+        NCCLCHK(h, ncclAllReduce(bufs[i], bufs[i], n, ncclUint64, ncclSum, s.comm_nccl,
+                                 s.compute));
+    }
+    NCCLCHK(h, ncclGroupEnd());
+    return GOLHIP_OK;
+}
+
+// Extraction of cell lists (alive cells: b == nullptr; flips: b = previous generation).
+int extract(golhip_t h, bool flips, int32_t *xy, size_t cap, size_t *n) {
+    if (!n) return fail(h, GOLHIP_ERR_ARG, "n is null");
+    if (flips && !h->prev_valid)
+        return fail(h, GOLHIP_ERR_STATE,
+                    "flips need the previous generation: step by 1 turn (k-blocked launches "
+                    "keep only the newest generation)");
+    size_t total = 0;
+    std::vector<unsigned long long> shard_totals(h->shards.size());
+    std::vector<std::pair<uint32_t *, unsigned long long *>> scratch(h->shards.size());
+    for (size_t i = 0; i < h->shards.size(); ++i) {
+        Shard &s = h->shards[i];
+        HIPCHK(h, hipSetDevice(s.device));
+        uint32_t *rc = nullptr;
+        unsigned long long *off = nullptr;
+        HIPCHK(h, hipMalloc(&rc, sizeof(uint32_t) * (size_t)s.rows));
+        HIPCHK(h, hipMalloc(&off, sizeof(unsigned long long) * (size_t)(s.rows + 1)));
+        scratch[i] = {rc, off};
+        const uint32_t *a = h->row0(s, h->cur);
+        const uint32_t *b = flips ? h->row0(s, h->cur ^ 1) : nullptr;
+        HIPCHK(h, golhip::launch_extract_count(a, b, h->pitch, s.rows, h->width, rc, off,
+                                               s.compute));
+        HIPCHK(h, hipMemcpyAsync(&shard_totals[i], off + s.rows, sizeof(unsigned long long),
+                                 hipMemcpyDeviceToHost, s.compute));
+    }
+    for (size_t i = 0; i < h->shards.size(); ++i) {
+        HIPCHK(h, hipSetDevice(h->shards[i].device));
+        HIPCHK(h, hipStreamSynchronize(h->shards[i].compute));
+        total += shard_totals[i];
+    }
+    *n = total;
+    int ret = GOLHIP_OK;
+    if (total > cap) {
+        ret = fail(h, GOLHIP_ERR_CAP, "%zu cells do not fit in cap %zu", total, cap);
+    } else if (total > 0) {
+        if (!xy) return fail(h, GOLHIP_ERR_ARG, "xy is null");
+        size_t base = 0;
+        for (size_t i = 0; i < h->shards.size(); ++i) {
+            Shard &s = h->shards[i];
+            const size_t cnt = shard_totals[i];
+            HIPCHK(h, hipSetDevice(s.device));
+            if (cnt) {
+                int32_t *dxy = nullptr;
+                HIPCHK(h, hipMalloc(&dxy, sizeof(int32_t) * 2 * cnt));
+                const uint32_t *a = h->row0(s, h->cur);
+                const uint32_t *b = flips ? h->row0(s, h->cur ^ 1) : nullptr;
+                HIPCHK(h, golhip::launch_extract_emit(a, b, h->pitch, s.rows, h->width,
+                                                      scratch[i].second, s.y0, dxy, cnt,
+                                                      s.compute));
+                HIPCHK(h, hipMemcpyAsync(xy + 2 * base, dxy, sizeof(int32_t) * 2 * cnt,
+                                         hipMemcpyDeviceToHost, s.compute));
+                HIPCHK(h, hipStreamSynchronize(s.compute));
+                HIPCHK(h, hipFree(dxy));
+            }
+            base += cnt;
+        }
+    }
+    for (size_t i = 0; i < h->shards.size(); ++i) {
+        HIPCHK(h, hipSetDevice(h->shards[i].device));
+        HIPCHK(h, hipStreamSynchronize(h->shards[i].compute));
+        HIPCHK(h, hipFree(scratch[i].first));
+        HIPCHK(h, hipFree(scratch[i].second));
+    }
+    return ret;
+}
+
+// Host <-> device byte transfer of the handle's rows, in row chunks of <= 64 MiB staging.
+int transfer_bytes(golhip_t h, uint8_t *host, size_t row_stride, bool to_device) {
+    if (!host) return fail(h, GOLHIP_ERR_ARG, "buffer is null");
+    if (row_stride < (size_t)h->width) return fail(h, GOLHIP_ERR_ARG, "row_stride < width");
+    const int64_t W = h->width;
+    const int64_t chunk_rows = std::max<int64_t>(1, (64ll << 20) / W);
+    int64_t hrow = 0;  // host row index relative to the handle's first row
+    for (auto &s : h->shards) {
+        HIPCHK(h, hipSetDevice(s.device));
+        uint8_t *stage = nullptr;
+        const int64_t cr = std::min(chunk_rows, s.rows);
+        HIPCHK(h, hipMalloc(&stage, (size_t)(cr * W)));
+        for (int64_t y = 0; y < s.rows; y += cr) {
+            const int64_t nr = std::min(cr, s.rows - y);
+            uint32_t *rows_dev = h->row0(s, h->cur) + y * h->pitch;
+            if (to_device) {
+                HIPCHK(h, hipMemcpy2DAsync(stage, (size_t)W, host + (size_t)(hrow + y) * row_stride,
+                                           row_stride, (size_t)W, (size_t)nr,
+                                           hipMemcpyHostToDevice, s.compute));
+                HIPCHK(h, golhip::launch_pack(stage, nr, W, h->wd, rows_dev, h->pitch, s.compute));
+            } else {
+                HIPCHK(h, golhip::launch_unpack(rows_dev, h->pitch, nr, W, stage, s.compute));
+                HIPCHK(h, hipMemcpy2DAsync(host + (size_t)(hrow + y) * row_stride, row_stride,
+                                           stage, (size_t)W, (size_t)W, (size_t)nr,
+                                           hipMemcpyDeviceToHost, s.compute));
+            }
+            HIPCHK(h, hipStreamSynchronize(s.compute));
+        }
+        HIPCHK(h, hipFree(stage));
+        hrow += s.rows;
+    }
+    return GOLHIP_OK;
+}
+
+int create_common(golhip_t h) {
+    for (auto &s : h->shards) {
+        int rc = alloc_shard(h, s);
+        if (rc) return rc;
+    }
+    return GOLHIP_OK;
+}
+
+}  // namespace
+
+// ================================================================================ C ABI ====
+extern "C" {
+
+int golhip_version(void) { return kVersion; }
+
+const char *golhip_strerror(int code) {
+    switch (code) {
+        case GOLHIP_OK: return "ok";
+        case GOLHIP_ERR_ARG: return "invalid argument";
+        case GOLHIP_ERR_HIP: return "HIP runtime error";
+        case GOLHIP_ERR_OOM: return "out of device memory";
+        case GOLHIP_ERR_CAP: return "output capacity too small";
+        case GOLHIP_ERR_RCCL: return "RCCL error";
+        case GOLHIP_ERR_NODEV: return "no usable gfx950 device";
+        case GOLHIP_ERR_STATE: return "invalid state for this call";
+        default: return "unknown error";
+    }
+}
+
+int golhip_device_count(int *out) {
+    if (!out) return GOLHIP_ERR_ARG;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *out = n;
+    return GOLHIP_OK;
+}
+
+int golhip_strip_bounds(int64_t height, int world_size, int rank, int64_t *y0, int64_t *rows) {
+    if (height <= 0 || world_size <= 0 || rank < 0 || rank >= world_size || !y0 || !rows)
+        return GOLHIP_ERR_ARG;
+    strip_bounds(height, world_size, rank, *y0, *rows);
+    return GOLHIP_OK;
+}
+
+int golhip_nccl_unique_id(uint8_t *out) {
+    if (!out) return GOLHIP_ERR_ARG;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return GOLHIP_ERR_RCCL;
+    static_assert(sizeof(ncclUniqueId) == GOLHIP_NCCL_ID_BYTES, "nccl id size");
+    std::memcpy(out, &id, sizeof id);
+    return GOLHIP_OK;
+}
+
+int golhip_create(int width, int height, int ngpus, int k, golhip_t *out) {
+    if (!out) return GOLHIP_ERR_ARG;
+    *out = nullptr;
+    int rc = validate_geometry(width, height, ngpus, k);
+    if (rc) return rc;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < ngpus) return GOLHIP_ERR_NODEV;
+    golhip_t h = new golhip_engine();
+    setup_engine(h, width, height, ngpus, k);
+    h->shards.resize(ngpus);
+    for (int r = 0; r < ngpus; ++r) {
+        Shard &s = h->shards[r];
+        s.device = r;
+        s.rank = r;
+        strip_bounds(height, ngpus, r, s.y0, s.rows);
+        if ((rc = check_device_arch(h, r))) goto fail;
+    }
+    if ((rc = create_common(h))) goto fail;
+    if (ngpus > 1) {
+        std::vector<ncclComm_t> comms(ngpus);
+        std::vector<int> devs(ngpus);
+        std::iota(devs.begin(), devs.end(), 0);
+        if (ncclCommInitAll(comms.data(), ngpus, devs.data()) != ncclSuccess) {
+            rc = GOLHIP_ERR_RCCL;
+            goto fail;
+        }
+        for (int r = 0; r < ngpus; ++r) h->shards[r].comm_nccl = comms[r];
+    }
+    *out = h;
+    return GOLHIP_OK;
+fail:
+    for (auto &s : h->shards) free_shard(s);
+    delete h;
+    return rc;
+}
+
+int golhip_create_rank(int width, int height, int rank, int world_size, int device, int k,
+                       const uint8_t *nccl_id, golhip_t *out) {
+    if (!out) return GOLHIP_ERR_ARG;
+    *out = nullptr;
+    int rc = validate_geometry(width, height, world_size, k);
+    if (rc) return rc;
+    if (rank < 0 || rank >= world_size || device < 0) return GOLHIP_ERR_ARG;
+    if (world_size > 1 && !nccl_id) return GOLHIP_ERR_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) return GOLHIP_ERR_NODEV;
+    golhip_t h = new golhip_engine();
+    setup_engine(h, width, height, world_size, k);
+    h->rank_mode = true;
+    h->shards.resize(1);
+    Shard &s = h->shards[0];
+    s.device = device;
+    s.rank = rank;
+    strip_bounds(height, world_size, rank, s.y0, s.rows);
+    if ((rc = check_device_arch(h, device))) goto fail;
+    if ((rc = create_common(h))) goto fail;
+    if (world_size > 1) {
+        ncclUniqueId id;
+        std::memcpy(&id, nccl_id, sizeof id);
+        (void)hipSetDevice(device);
+        if (ncclCommInitRank(&s.comm_nccl, world_size, id, rank) != ncclSuccess) {
+            rc = GOLHIP_ERR_RCCL;
+            goto fail;
+        }
+    }
+    *out = h;
+    return GOLHIP_OK;
+fail:
+    for (auto &sh : h->shards) free_shard(sh);
+    delete h;
+    return rc;
+}
+
+int golhip_destroy(golhip_t h) {
+    if (!h) return GOLHIP_ERR_ARG;
+    for (auto &tp : h->tpool) {
+        (void)hipEventDestroy(tp.a);
+        (void)hipEventDestroy(tp.b);
+    }
+    for (auto &s : h->shards) free_shard(s);
+    delete h;
+    return GOLHIP_OK;
+}
+
+const char *golhip_last_error(golhip_t h) { return h ? h->err.c_str() : "null handle"; }
+
+int golhip_get_info(golhip_t h, golhip_info *out) {
+    if (!h || !out) return GOLHIP_ERR_ARG;
+    out->width = h->width;
+    out->height = h->height;
+    out->torus_width = h->L;
+    out->y0 = h->shards.front().y0;
+    int64_t rows = 0;
+    for (auto &s : h->shards) rows += s.rows;
+    out->rows = rows;
+    out->rank = h->shards.front().rank;
+    out->world_size = h->world_size;
+    out->nshards = (int32_t)h->shards.size();
+    out->k = h->k;
+    out->halo_rows = h->halo;
+    out->band_rows = h->band_rows;
+    return GOLHIP_OK;
+}
+
+int golhip_load_bytes(golhip_t h, const uint8_t *cells, size_t row_stride) {
+    if (!h) return GOLHIP_ERR_ARG;
+    int rc = sync_all(h);
+    if (rc) return rc;
+    rc = transfer_bytes(h, const_cast<uint8_t *>(cells), row_stride, true);
+    if (rc) return rc;
+    h->turn = 0;
+    h->prev_valid = false;
+    return GOLHIP_OK;
+}
+
+int golhip_store_bytes(golhip_t h, uint8_t *out, size_t row_stride) {
+    if (!h) return GOLHIP_ERR_ARG;
+    int rc = sync_all(h);
+    if (rc) return rc;
+    return transfer_bytes(h, out, row_stride, false);
+}
+
+int golhip_init_random(golhip_t h, uint64_t seed, uint32_t density_q32) {
+    if (!h) return GOLHIP_ERR_ARG;
+    if (h->width % 64 != 0) return fail(h, GOLHIP_ERR_ARG, "init_random needs width %% 64 == 0");
+    for (auto &s : h->shards) {
+        HIPCHK(h, hipSetDevice(s.device));
+        HIPCHK(h, golhip::launch_init_random(h->row0(s, h->cur), h->pitch, s.rows, s.y0, h->width,
+                                             h->wd, seed, density_q32, s.compute));
+    }
+    h->turn = 0;
+    h->prev_valid = false;
+    return sync_all(h);
+}
+
+int golhip_store_words(golhip_t h, uint64_t *out) {
+    if (!h || !out) return GOLHIP_ERR_ARG;
+    if (h->width % 64 != 0) return fail(h, GOLHIP_ERR_ARG, "store_words needs width %% 64 == 0");
+    int rc = sync_all(h);
+    if (rc) return rc;
+    const int64_t wpr = h->width / 64;
+    int64_t hrow = 0;
+    for (auto &s : h->shards) {
+        HIPCHK(h, hipSetDevice(s.device));
+        uint64_t *d = nullptr;
+        HIPCHK(h, hipMalloc(&d, sizeof(uint64_t) * (size_t)(s.rows * wpr)));
+        HIPCHK(h, golhip::launch_words_out(h->row0(s, h->cur), h->pitch, s.rows, h->width, d,
+                                           s.compute));
+        HIPCHK(h, hipMemcpyAsync(out + hrow * wpr, d, sizeof(uint64_t) * (size_t)(s.rows * wpr),
+                                 hipMemcpyDeviceToHost, s.compute));
+        HIPCHK(h, hipStreamSynchronize(s.compute));
+        HIPCHK(h, hipFree(d));
+        hrow += s.rows;
+    }
+    return GOLHIP_OK;
+}
+
+int golhip_load_words(golhip_t h, const uint64_t *in) {
+    if (!h || !in) return GOLHIP_ERR_ARG;
+    if (h->width % 64 != 0) return fail(h, GOLHIP_ERR_ARG, "load_words needs width %% 64 == 0");
+    int rc = sync_all(h);
+    if (rc) return rc;
+    const int64_t wpr = h->width / 64;
+    int64_t hrow = 0;
+    for (auto &s : h->shards) {
+        HIPCHK(h, hipSetDevice(s.device));
+        uint64_t *d = nullptr;
+        HIPCHK(h, hipMalloc(&d, sizeof(uint64_t) * (size_t)(s.rows * wpr)));
+        HIPCHK(h, hipMemcpyAsync(d, in + hrow * wpr, sizeof(uint64_t) * (size_t)(s.rows * wpr),
+                                 hipMemcpyHostToDevice, s.compute));
+        HIPCHK(h, golhip::launch_words_in(d, s.rows, h->width, h->wd, h->row0(s, h->cur),
+                                          h->pitch, s.compute));
+        HIPCHK(h, hipStreamSynchronize(s.compute));
+        HIPCHK(h, hipFree(d));
+        hrow += s.rows;
+    }
+    h->turn = 0;
+    h->prev_valid = false;
+    return GOLHIP_OK;
+}
+
+int golhip_step(golhip_t h, int64_t turns, uint64_t *alive_per_turn) {
+    if (!h || turns < 0) return GOLHIP_ERR_ARG;
+    if (turns == 0) return GOLHIP_OK;
+    const bool counting = alive_per_turn != nullptr;
+    if (counting) {
+        for (auto &s : h->shards) {
+            if (s.d_counts_cap < (size_t)turns) {
+                HIPCHK(h, hipSetDevice(s.device));
+                HIPCHK(h, hipStreamSynchronize(s.compute));
+                if (s.d_counts) HIPCHK(h, hipFree(s.d_counts));
+                s.d_counts = nullptr;
+                HIPCHK(h, hipMalloc(&s.d_counts, sizeof(unsigned long long) * (size_t)turns));
+                s.d_counts_cap = (size_t)turns;
+            }
+        }
+    }
+    int64_t done = 0;
+    while (done < turns) {
+        const int64_t left = turns - done;
+        const int K = pick_k((int)std::min<int64_t>(left, h->k));
+        int rc = step_block(h, K, counting ? done : -1);
+        if (rc) return rc;
+        done += K;
+    }
+    if (counting) {
+        std::vector<unsigned long long *> bufs;
+        for (auto &s : h->shards) bufs.push_back(s.d_counts);
+        // sum the strips of this handle on shard 0 (single-process multi-GPU) ...
+        int rc = allreduce_u64(h, bufs, (size_t)turns);  // ... and over ranks
+        if (rc) return rc;
+        Shard &s0 = h->shards[0];
+        HIPCHK(h, hipSetDevice(s0.device));
+        HIPCHK(h, hipMemcpyAsync(alive_per_turn, s0.d_counts, sizeof(uint64_t) * (size_t)turns,
+                                 hipMemcpyDeviceToHost, s0.compute));
+        HIPCHK(h, hipStreamSynchronize(s0.compute));
+        const uint64_t rep = (uint64_t)h->rep();
+        if (rep > 1)
+            for (int64_t i = 0; i < turns; ++i) alive_per_turn[i] /= rep;
+    }
+    return GOLHIP_OK;
+}
+
+int golhip_alive_count(golhip_t h, uint64_t *out) {
+    if (!h || !out) return GOLHIP_ERR_ARG;
+    std::vector<unsigned long long *> bufs;
+    for (auto &s : h->shards) {
+        HIPCHK(h, hipSetDevice(s.device));
+        HIPCHK(h, hipMemsetAsync(s.scratch_u64, 0, sizeof(unsigned long long), s.compute));
+        HIPCHK(h, golhip::launch_popcount(h->row0(s, h->cur), h->pitch, s.rows, h->wd,
+                                          s.scratch_u64, s.compute));
+        bufs.push_back(s.scratch_u64);
+    }
+    int rc = allreduce_u64(h, bufs, 1);
+    if (rc) return rc;
+    unsigned long long v = 0;
+    Shard &s0 = h->shards[0];
+    HIPCHK(h, hipSetDevice(s0.device));
+    HIPCHK(h, hipMemcpyAsync(&v, s0.scratch_u64, sizeof v, hipMemcpyDeviceToHost, s0.compute));
+    HIPCHK(h, hipStreamSynchronize(s0.compute));
+    *out = v / (unsigned long long)h->rep();
+    return GOLHIP_OK;
+}
+
+int golhip_alive_cells(golhip_t h, int32_t *xy, size_t cap, size_t *n) {
+    if (!h) return GOLHIP_ERR_ARG;
+    int rc = sync_all(h);
+    if (rc) return rc;
+    return extract(h, false, xy, cap, n);
+}
+
+int golhip_flips(golhip_t h, int32_t *xy, size_t cap, size_t *n) {
+    if (!h) return GOLHIP_ERR_ARG;
+    int rc = sync_all(h);
+    if (rc) return rc;
+    return extract(h, true, xy, cap, n);
+}
+
+int golhip_turn(golhip_t h, int64_t *out) {
+    if (!h || !out) return GOLHIP_ERR_ARG;
+    *out = h->turn;
+    return GOLHIP_OK;
+}
+
+int golhip_set_turn(golhip_t h, int64_t turn) {
+    if (!h || turn < 0) return GOLHIP_ERR_ARG;
+    h->turn = turn;
+    return GOLHIP_OK;
+}
+
+int golhip_set_k(golhip_t h, int k) {
+    if (!h) return GOLHIP_ERR_ARG;
+    if (k < 1 || k > golhip::kMaxK) return fail(h, GOLHIP_ERR_ARG, "k must be 1..%d", golhip::kMaxK);
+    if (h->world_size > 1 && k > h->halo)
+        return fail(h, GOLHIP_ERR_ARG, "k=%d exceeds the %d halo rows allocated at create", k,
+                    h->halo);
+    h->k = k;
+    return GOLHIP_OK;
+}
+
+int golhip_set_band_rows(golhip_t h, int band_rows) {
+    if (!h || band_rows < 0) return GOLHIP_ERR_ARG;
+    h->band_rows = band_rows;
+    return GOLHIP_OK;
+}
+
+int golhip_sync(golhip_t h) {
+    if (!h) return GOLHIP_ERR_ARG;
+    return sync_all(h);
+}
+
+int golhip_timing(golhip_t h, int enable) {
+    if (!h) return GOLHIP_ERR_ARG;
+    int rc = timing_collect(h);
+    if (rc) return rc;
+    h->timing = enable != 0;
+    h->tms = 0.0;
+    h->tlaunches = 0;
+    h->tgens = 0;
+    return GOLHIP_OK;
+}
+
+int golhip_kernel_time(golhip_t h, double *total_ms, int64_t *launches, int64_t *generations) {
+    if (!h) return GOLHIP_ERR_ARG;
+    int rc = timing_collect(h);
+    if (rc) return rc;
+    if (total_ms) *total_ms = h->tms;
+    if (launches) *launches = h->tlaunches;
+    if (generations) *generations = h->tgens;
+    return GOLHIP_OK;
+}
+
+}  // extern "C"

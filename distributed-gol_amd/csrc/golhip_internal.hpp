@@ -1,0 +1,70 @@
+// golhip_internal.hpp -- launch-side interface between the engine (golhip_engine.hip) and the
+// gfx950 kernels (golhip_kernels.hip).  Not part of the public ABI (include/golhip.h is).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace golhip {
+
+// Device layout of one row strip (see DESIGN.md "Data layout in HBM"):
+//   torus width L = lcm(width, 128) bits, wd = L/32 uint32 words per row, LSB-first
+//   (bit b of word j is x = 32j+b; identical bytes to LSB-first uint64 words), rows
+//   contiguous at `pitch` words; `halo` extra rows above row 0 and below the last row.
+
+// Stencil launch: output rows [r0b, r0e) and [r1b, r1e) (second range may be empty) of the
+// strip after K generations, computed from the input strip.
+struct StencilParams {
+    int64_t pitch;       // words between consecutive rows
+    int64_t r0b, r0e;    // output range 0
+    int64_t r1b, r1e;    // output range 1 (r1b == r1e: none)
+    int64_t band;        // output rows per wave band
+    int64_t nbands0;     // bands in range 0
+    int64_t nbands;      // bands in total
+    int64_t wrap_rows;   // > 0: single strip holding the whole torus height (row index mod H)
+    int64_t lo, hi;      // halo mode: readable input rows [lo, hi) relative to row 0
+    int32_t wd;          // words per row of the torus
+    int32_t nchunks;     // 62-word column chunks per row (lanes 1..62 own, 0 and 63 are halo)
+};
+
+constexpr int kMaxK = 32;         // generations per launch limit (halo lane = 32 bits)
+constexpr int kCountSlots = 64;   // per-generation count slots (spread the atomics)
+
+// Launch the K-generation stencil (K in {1,2,4,8,16,32}). count_slots (nullable) receives
+// per-generation alive counts in kCountSlots slots per generation.
+hipError_t launch_stencil(int K, const uint32_t *in_row0, uint32_t *out_row0,
+                          const StencilParams &p, unsigned long long *count_slots,
+                          hipStream_t s);
+bool stencil_k_supported(int K);
+// Sum the slots of K generations into counts[0..K) and zero the slots.
+hipError_t launch_count_finalize(int K, unsigned long long *slots, unsigned long long *counts,
+                                 hipStream_t s);
+
+// 0/nonzero bytes (rows x width, compact, stride == width) -> packed torus rows.
+hipError_t launch_pack(const uint8_t *bytes, int64_t rows, int64_t width, int32_t wd,
+                       uint32_t *row0, int64_t pitch, hipStream_t s);
+// First `width` columns of packed rows -> 0/255 bytes (compact, stride == width).
+hipError_t launch_unpack(const uint32_t *row0, int64_t pitch, int64_t rows, int64_t width,
+                         uint8_t *bytes, hipStream_t s);
+// Counter-based random rows; gy0 = global index of local row 0.
+hipError_t launch_init_random(uint32_t *row0, int64_t pitch, int64_t rows, int64_t gy0,
+                              int64_t width, int32_t wd, uint64_t seed, uint32_t density_q32,
+                              hipStream_t s);
+// Popcount of rows x wd words, added into *out.
+hipError_t launch_popcount(const uint32_t *row0, int64_t pitch, int64_t rows, int32_t wd,
+                           unsigned long long *out, hipStream_t s);
+// Alive-cell / flip extraction (row-major): cells are bits of (a ^ b) (b nullable) in the first
+// `width` columns.  row_counts[rows], offsets[rows+1] are scratch; offsets[rows] = total.
+hipError_t launch_extract_count(const uint32_t *a, const uint32_t *b, int64_t pitch,
+                                int64_t rows, int64_t width, uint32_t *row_counts,
+                                unsigned long long *offsets, hipStream_t s);
+hipError_t launch_extract_emit(const uint32_t *a, const uint32_t *b, int64_t pitch,
+                               int64_t rows, int64_t width, const unsigned long long *offsets,
+                               int64_t gy0, int32_t *xy, uint64_t cap, hipStream_t s);
+// Packed torus rows <-> logical uint64 words (width % 64 == 0; first width bits of each row).
+hipError_t launch_words_out(const uint32_t *row0, int64_t pitch, int64_t rows, int64_t width,
+                            uint64_t *words, hipStream_t s);
+hipError_t launch_words_in(const uint64_t *words, int64_t rows, int64_t width, int32_t wd,
+                           uint32_t *row0, int64_t pitch, hipStream_t s);
+
+}  // namespace golhip

@@ -1,0 +1,547 @@
+// golhip_kernels.hip -- hand-written gfx950 (CDNA4, wave64) kernels of libgolhip.
+//
+// Hot path: gol_stencil<K>, a temporally blocked, bit-sliced B3/S23 stencil on a 1-bit-per-cell
+// torus.  It replaces the reference's per-cell worker loop
+//   calculateNextState / updateCell / countAliveCellsAdjacent   server/server.go:21-75
+// and the per-turn alive scan calculateAliveCells (gol/distributor.go:153-166,186) is fused into
+// it as a per-generation popcount.
+//
+// Mapping (see DESIGN.md for the roofline):
+//   * one lane = one 32-bit word (32 cells) of a row; a wave = 64 consecutive words of a row:
+//     lanes 1..62 own their word, lanes 0 and 63 are horizontal halo (their outer bits go stale
+//     one bit per generation, so K <= 32 keeps every owned bit exact);
+//   * horizontal neighbours cross lanes with DPP wave_shr:1 / wave_shl:1 and are merged with
+//     v_alignbit; the 9-cell sums use v_bitop3 (gfx950) full adders;
+//   * each wave streams down a band of rows keeping, per generation level, the last two rows'
+//     (sum, carry, cell) in registers: one input row in -> one row out per level per step, so a
+//     launch advances K generations while reading the board once and writing it once.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "golhip_internal.hpp"
+
+namespace golhip {
+namespace {
+
+__device__ __forceinline__ uint32_t lane_from_west(uint32_t v) {  // lane i <- lane i-1
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138 /* wave_shr:1 */, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t lane_from_east(uint32_t v) {  // lane i <- lane i+1
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130 /* wave_shl:1 */, 0xf, 0xf, false);
+}
+
+// v_bitop3_b32 (gfx950): any 3-input boolean function in one VALU op.  The immediate is the
+// truth table indexed by (s0 << 2) | (s1 << 1) | s2, i.e. f(0xF0, 0xCC, 0xAA).
+#define GOL_TT(EXPR) ((uint8_t)([](uint32_t a, uint32_t b, uint32_t c) { return (EXPR); }(0xF0u, 0xCCu, 0xAAu)))
+#define GOL_BOP3(A, B, C, TT) __builtin_amdgcn_bitop3_b32((A), (B), (C), (TT))
+constexpr uint8_t kXor3 = GOL_TT(a ^ b ^ c);                          // 0x96
+constexpr uint8_t kMaj = GOL_TT((a & b) | (c & (a | b)));             // 0xE8
+constexpr uint8_t kTwosIs1 = GOL_TT((a ^ b) & ~c);                    // p, k, q -> T == 1
+constexpr uint8_t kTwosIs2 = GOL_TT((c & ~(a | b)) | (~c & a & b));   // p, k, q -> T == 2
+constexpr uint8_t kSelect = GOL_TT((a & b) | (~a & c));               // a ? b : c
+
+// Horizontal 3-cell sum of a row word c (west + self + east) as sum bit s and carry cy.
+__device__ __forceinline__ void row_sum3(uint32_t c, uint32_t &s, uint32_t &cy) {
+    const uint32_t wl = lane_from_west(c), el = lane_from_east(c);
+    const uint32_t w = __builtin_amdgcn_alignbit(c, wl, 31);  // cell x-1 moved onto x
+    const uint32_t e = __builtin_amdgcn_alignbit(el, c, 1);   // cell x+1 moved onto x
+    s = GOL_BOP3(w, c, e, kXor3);
+    cy = GOL_BOP3(w, c, e, kMaj);
+}
+
+// B3/S23 from three rows' 3-cell sums: S9 = 9-cell sum including the centre cell mc;
+// alive next iff S9 == 3, or S9 == 4 and the cell is alive (server/server.go:35-52).
+// 8 VALU ops (7 v_bitop3 + 1 v_and).
+__device__ __forceinline__ uint32_t life_next(uint32_t as, uint32_t acy, uint32_t ms,
+                                              uint32_t mcy, uint32_t mc, uint32_t bs,
+                                              uint32_t bcy) {
+    const uint32_t o = GOL_BOP3(as, ms, bs, kXor3);    // S9 bit 0
+    const uint32_t k = GOL_BOP3(as, ms, bs, kMaj);     // carry into the twos
+    const uint32_t p = GOL_BOP3(acy, mcy, bcy, kXor3);
+    const uint32_t q = GOL_BOP3(acy, mcy, bcy, kMaj);
+    // T = S9 >> 1 = p + 2q + k
+    const uint32_t t1 = GOL_BOP3(p, k, q, kTwosIs1);   // T == 1  (S9 == 3 when o)
+    const uint32_t t2 = GOL_BOP3(p, k, q, kTwosIs2);   // T == 2  (S9 == 4 when !o)
+    return GOL_BOP3(o, t1, mc & t2, kSelect);
+}
+
+template <int K, bool COUNT>
+__global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ in,
+                                                   uint32_t *__restrict__ out, StencilParams p,
+                                                   unsigned long long *__restrict__ slots) {
+    const int lane = threadIdx.x & 63;
+    // wave index made provably uniform so every band/row quantity lives in SGPRs
+    const int64_t wave =
+        (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int64_t chunk = wave % p.nchunks;
+    const int64_t bandi = wave / p.nchunks;
+    if (bandi >= p.nbands) return;  // wave-uniform
+    int64_t ya, yb;
+    if (bandi < p.nbands0) {
+        ya = p.r0b + bandi * p.band;
+        yb = min(ya + p.band, p.r0e);
+    } else {
+        ya = p.r1b + (bandi - p.nbands0) * p.band;
+        yb = min(ya + p.band, p.r1e);
+    }
+    const int colraw = (int)chunk * 62 + lane - 1;
+    const int col = (colraw + p.wd) % p.wd;
+    const bool owned = lane >= 1 && lane <= 62 && colraw < p.wd;
+
+    // Input row stream: rows ya-K, ya-K+1, ... (wrap mod H, or clamped to the halo'd strip).
+    // Row pointers are wave-uniform (SGPRs); the lane adds its column.
+    int64_t ly = ya - K;
+    if (p.wrap_rows > 0) {
+        ly %= p.wrap_rows;
+        if (ly < 0) ly += p.wrap_rows;
+    } else {
+        ly = ly < p.lo ? p.lo : (ly >= p.hi ? p.hi - 1 : ly);
+    }
+    const uint32_t *lrow = in + ly * p.pitch;
+    auto load_next = [&]() -> uint32_t {
+        const uint32_t v = lrow[col];
+        if (p.wrap_rows > 0) {
+            if (++ly == p.wrap_rows) {
+                ly = 0;
+                lrow = in;
+            } else {
+                lrow += p.pitch;
+            }
+        } else if (ly + 1 < p.hi) {
+            ++ly;
+            lrow += p.pitch;
+        }
+        return v;
+    };
+    uint32_t *orow = out + ya * p.pitch;
+
+    // Per-level two-slot ring of (sum, carry, cell) rows; X/Y swap roles every step.
+    uint32_t xs[K], xcy[K], xc[K], ys[K], ycy[K], yc[K], acc[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        xs[j] = xcy[j] = xc[j] = ys[j] = ycy[j] = yc[j] = 0;
+        acc[j] = 0;
+    }
+    const int64_t nrows = yb - ya;
+    const int64_t nsteps = nrows + 2 * K;
+
+    // One step: a new level-0 row enters, every level emits one row; the level-K row is stored.
+    // PAR 0: above = X, mid = Y, new -> X.  PAR 1: above = Y, mid = X, new -> Y.
+#define GOL_STEP(PAR, VIN, SI)                                                              \
+    do {                                                                                    \
+        uint32_t nc = (VIN);                                                                \
+        const int64_t st = (SI);                                                            \
+        _Pragma("unroll") for (int j = 0; j < K; ++j) {                                     \
+            uint32_t ns, ncy;                                                               \
+            row_sum3(nc, ns, ncy);                                                          \
+            uint32_t nx;                                                                    \
+            if (PAR == 0) {                                                                 \
+                nx = life_next(xs[j], xcy[j], ys[j], ycy[j], yc[j], ns, ncy);               \
+                xs[j] = ns; xcy[j] = ncy; xc[j] = nc;                                       \
+            } else {                                                                        \
+                nx = life_next(ys[j], ycy[j], xs[j], xcy[j], xc[j], ns, ncy);               \
+                ys[j] = ns; ycy[j] = ncy; yc[j] = nc;                                       \
+            }                                                                               \
+            if (COUNT) {                                                                    \
+                const int64_t r = st - K - (j + 1); /* level j+1 row - ya */                \
+                if (r >= 0 && r < nrows) acc[j] += __builtin_popcount(nx);                  \
+            }                                                                               \
+            nc = nx;                                                                        \
+        }                                                                                   \
+        if (st >= 2 * K && st - 2 * K < nrows) {                                            \
+            if (owned) orow[col] = nc;                                                      \
+            orow += p.pitch;                                                                \
+        }                                                                                   \
+    } while (0)
+
+    uint32_t b0 = load_next(), b1 = load_next(), b2 = load_next(), b3 = load_next();
+    for (int64_t s = 0; s < nsteps; s += 4) {
+        GOL_STEP(0, b0, s);
+        b0 = load_next();
+        GOL_STEP(1, b1, s + 1);
+        b1 = load_next();
+        GOL_STEP(0, b2, s + 2);
+        b2 = load_next();
+        GOL_STEP(1, b3, s + 3);
+        b3 = load_next();
+    }
+#undef GOL_STEP
+
+    if (COUNT) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            uint32_t v = owned ? acc[j] : 0u;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+            if (lane == 0 && v)
+                atomicAdd(&slots[j * kCountSlots + (int)(wave & (kCountSlots - 1))],
+                          (unsigned long long)v);
+        }
+    }
+}
+
+__global__ void count_finalize(int K, unsigned long long *slots, unsigned long long *counts) {
+    const int j = threadIdx.x;
+    if (j >= K) return;
+    unsigned long long s = 0;
+    for (int i = 0; i < kCountSlots; ++i) {
+        s += slots[j * kCountSlots + i];
+        slots[j * kCountSlots + i] = 0;
+    }
+    counts[j] = s;
+}
+
+// ------------------------------------------------------------------ board I/O (gol/io.go)
+__global__ void pack_rows(const uint8_t *__restrict__ bytes, int64_t rows, int64_t width,
+                          int32_t wd, uint32_t *__restrict__ row0, int64_t pitch) {
+    const int64_t n = rows * wd;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t y = i / wd;
+        const int32_t col = (int32_t)(i - y * wd);
+        const uint8_t *r = bytes + y * width;
+        uint32_t v = 0;
+        if ((width & 31) == 0) {
+            const int64_t x0 = ((int64_t)col * 32) % width;
+            const uint4 *q = reinterpret_cast<const uint4 *>(r + x0);
+            const uint4 lo = q[0], hi = q[1];
+            const uint32_t w8[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    v |= (uint32_t)(((w8[k] >> (8 * b)) & 0xffu) != 0) << (4 * k + b);
+        } else {
+            for (int b = 0; b < 32; ++b) {
+                const int64_t x = ((int64_t)col * 32 + b) % width;
+                v |= (uint32_t)(r[x] != 0) << b;
+            }
+        }
+        row0[y * pitch + col] = v;
+    }
+}
+
+__global__ void unpack_rows(const uint32_t *__restrict__ row0, int64_t pitch, int64_t rows,
+                            int64_t width, uint8_t *__restrict__ bytes) {
+    if ((width & 15) == 0) {
+        const int64_t per_row = width / 16, n = rows * per_row;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+             i += (int64_t)gridDim.x * blockDim.x) {
+            const int64_t y = i / per_row, t = i - y * per_row, x0 = t * 16;
+            const uint32_t bits = (row0[y * pitch + (x0 >> 5)] >> (x0 & 31)) & 0xffffu;
+            uint32_t o[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                uint32_t w = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) w |= (((bits >> (4 * k + b)) & 1u) * 0xffu) << (8 * b);
+                o[k] = w;
+            }
+            *reinterpret_cast<uint4 *>(bytes + y * width + x0) = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+    } else {
+        const int64_t n = rows * width;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+             i += (int64_t)gridDim.x * blockDim.x) {
+            const int64_t y = i / width, x = i - y * width;
+            bytes[i] = ((row0[y * pitch + (x >> 5)] >> (x & 31)) & 1u) ? 255 : 0;
+        }
+    }
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+__global__ void init_random_rows(uint32_t *__restrict__ row0, int64_t pitch, int64_t rows,
+                                 int64_t gy0, int64_t width, int32_t wd, uint64_t seed,
+                                 uint32_t density) {
+    const uint64_t g = 0x9E3779B97F4A7C15ULL;
+    const int64_t n = rows * wd, wpr = width / 64;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t y = i / wd;
+        const int32_t col = (int32_t)(i - y * wd);
+        const int64_t gy = gy0 + y;
+        const int64_t x0 = ((int64_t)col * 32) % width;
+        uint32_t v = 0;
+        if (density == 0x80000000u) {
+            const uint64_t wi = (uint64_t)gy * wpr + (uint64_t)(x0 >> 6);
+            const uint64_t w = splitmix64(seed + (wi + 1) * g);
+            v = (x0 & 32) ? (uint32_t)(w >> 32) : (uint32_t)w;
+        } else {
+            for (int b = 0; b < 32; ++b) {
+                const uint64_t c = (uint64_t)gy * width + (uint64_t)(x0 + b);
+                const uint32_t d = (uint32_t)splitmix64(seed + (c + 1) * g);
+                v |= (uint32_t)(d < density) << b;
+            }
+        }
+        row0[y * pitch + col] = v;
+    }
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+__global__ void popcount_rows(const uint32_t *__restrict__ row0, int64_t pitch, int64_t rows,
+                              int32_t wd, unsigned long long *__restrict__ out) {
+    __shared__ unsigned long long part[4];
+    const int64_t n = rows * wd;
+    unsigned long long c = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t y = i / wd;
+        c += __builtin_popcount(row0[y * pitch + (i - y * wd)]);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += part[w];
+        if (t) atomicAdd(out, t);
+    }
+}
+
+// ------------------------------------------------ alive-cell / flip extraction (row-major)
+__device__ __forceinline__ uint32_t cell_word(const uint32_t *a, const uint32_t *b,
+                                              int64_t off, int32_t col, int32_t nw,
+                                              uint32_t lastmask) {
+    uint32_t v = a[off];
+    if (b) v ^= b[off];
+    if (col == nw - 1) v &= lastmask;
+    return v;
+}
+
+__global__ void extract_count(const uint32_t *__restrict__ a, const uint32_t *__restrict__ b,
+                              int64_t pitch, int64_t rows, int32_t nw, uint32_t lastmask,
+                              uint32_t *__restrict__ row_counts) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t y = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); y < rows;
+         y += nwaves) {
+        uint32_t c = 0;
+        for (int32_t col = lane; col < nw; col += 64)
+            c += __builtin_popcount(cell_word(a, b, y * pitch + col, col, nw, lastmask));
+        c = wave_sum_u32(c);
+        if (lane == 0) row_counts[y] = c;
+    }
+}
+
+__global__ void extract_scan(const uint32_t *__restrict__ row_counts, int64_t rows,
+                             unsigned long long *__restrict__ offsets) {
+    __shared__ unsigned long long part[1024];
+    const int t = threadIdx.x, nt = blockDim.x;
+    const int64_t per = (rows + nt - 1) / nt, b0 = t * per, b1 = min(rows, b0 + per);
+    unsigned long long s = 0;
+    for (int64_t i = b0; i < b1; ++i) s += row_counts[i];
+    part[t] = s;
+    __syncthreads();
+    if (t == 0) {
+        unsigned long long run = 0;
+        for (int i = 0; i < nt; ++i) {
+            const unsigned long long x = part[i];
+            part[i] = run;
+            run += x;
+        }
+        offsets[rows] = run;
+    }
+    __syncthreads();
+    unsigned long long run = part[t];
+    for (int64_t i = b0; i < b1; ++i) {
+        offsets[i] = run;
+        run += row_counts[i];
+    }
+}
+
+__global__ void extract_emit(const uint32_t *__restrict__ a, const uint32_t *__restrict__ b,
+                             int64_t pitch, int64_t rows, int32_t nw, uint32_t lastmask,
+                             const unsigned long long *__restrict__ offsets, int64_t gy0,
+                             int32_t *__restrict__ xy, uint64_t cap) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t y = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); y < rows;
+         y += nwaves) {
+        unsigned long long base = offsets[y];
+        if (base >= cap) continue;
+        for (int32_t c0 = 0; c0 < nw; c0 += 64) {
+            const int32_t col = c0 + lane;
+            uint32_t v = col < nw ? cell_word(a, b, y * pitch + col, col, nw, lastmask) : 0u;
+            const uint32_t cnt = __builtin_popcount(v);
+            uint32_t incl = cnt;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t t = __shfl_up(incl, off, 64);
+                if (lane >= off) incl += t;
+            }
+            unsigned long long pos = base + (incl - cnt);
+            while (v) {
+                const int bit = __builtin_ctz(v);
+                v &= v - 1;
+                if (pos < cap) {
+                    xy[2 * pos] = col * 32 + bit;
+                    xy[2 * pos + 1] = (int32_t)(gy0 + y);
+                }
+                ++pos;
+            }
+            base += __shfl(incl, 63, 64);
+        }
+    }
+}
+
+__global__ void words_out(const uint32_t *__restrict__ row0, int64_t pitch, int64_t rows,
+                          int64_t wpr, uint64_t *__restrict__ words) {
+    const int64_t n = rows * wpr;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t y = i / wpr, j = i - y * wpr;
+        const uint32_t *r = row0 + y * pitch + 2 * j;
+        words[i] = (uint64_t)r[0] | ((uint64_t)r[1] << 32);
+    }
+}
+
+__global__ void words_in(const uint64_t *__restrict__ words, int64_t rows, int64_t wpr,
+                         int32_t wd, uint32_t *__restrict__ row0, int64_t pitch) {
+    const int64_t n = rows * wd;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t y = i / wd;
+        const int32_t col = (int32_t)(i - y * wd);
+        const int64_t lw = ((int64_t)col / 2) % wpr;  // logical word (torus replication)
+        const uint64_t w = words[y * wpr + lw];
+        row0[y * pitch + col] = (col & 1) ? (uint32_t)(w >> 32) : (uint32_t)w;
+    }
+}
+
+inline unsigned grid_for(int64_t n, int threads = 256, int64_t cap = 8192) {
+    int64_t g = (n + threads - 1) / threads;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (unsigned)g;
+}
+
+template <int K>
+hipError_t launch_stencil_k(const uint32_t *in, uint32_t *out, const StencilParams &p,
+                            unsigned long long *slots, hipStream_t s) {
+    const int64_t waves = p.nbands * (int64_t)p.nchunks;
+    const unsigned blocks = (unsigned)((waves + 3) / 4);
+    if (blocks == 0) return hipSuccess;
+    if (slots)
+        hipLaunchKernelGGL((gol_stencil<K, true>), dim3(blocks), dim3(256), 0, s, in, out, p,
+                           slots);
+    else
+        hipLaunchKernelGGL((gol_stencil<K, false>), dim3(blocks), dim3(256), 0, s, in, out, p,
+                           slots);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+bool stencil_k_supported(int K) {
+    return K == 1 || K == 2 || K == 4 || K == 8 || K == 16 || K == 32;
+}
+
+hipError_t launch_stencil(int K, const uint32_t *in_row0, uint32_t *out_row0,
+                          const StencilParams &p, unsigned long long *slots, hipStream_t s) {
+    switch (K) {
+        case 1: return launch_stencil_k<1>(in_row0, out_row0, p, slots, s);
+        case 2: return launch_stencil_k<2>(in_row0, out_row0, p, slots, s);
+        case 4: return launch_stencil_k<4>(in_row0, out_row0, p, slots, s);
+        case 8: return launch_stencil_k<8>(in_row0, out_row0, p, slots, s);
+        case 16: return launch_stencil_k<16>(in_row0, out_row0, p, slots, s);
+        case 32: return launch_stencil_k<32>(in_row0, out_row0, p, slots, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_count_finalize(int K, unsigned long long *slots, unsigned long long *counts,
+                                 hipStream_t s) {
+    hipLaunchKernelGGL(count_finalize, dim3(1), dim3(64), 0, s, K, slots, counts);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack(const uint8_t *bytes, int64_t rows, int64_t width, int32_t wd,
+                       uint32_t *row0, int64_t pitch, hipStream_t s) {
+    hipLaunchKernelGGL(pack_rows, dim3(grid_for(rows * wd)), dim3(256), 0, s, bytes, rows, width,
+                       wd, row0, pitch);
+    return hipGetLastError();
+}
+
+hipError_t launch_unpack(const uint32_t *row0, int64_t pitch, int64_t rows, int64_t width,
+                         uint8_t *bytes, hipStream_t s) {
+    const int64_t n = (width & 15) == 0 ? rows * (width / 16) : rows * width;
+    hipLaunchKernelGGL(unpack_rows, dim3(grid_for(n)), dim3(256), 0, s, row0, pitch, rows, width,
+                       bytes);
+    return hipGetLastError();
+}
+
+hipError_t launch_init_random(uint32_t *row0, int64_t pitch, int64_t rows, int64_t gy0,
+                              int64_t width, int32_t wd, uint64_t seed, uint32_t density_q32,
+                              hipStream_t s) {
+    hipLaunchKernelGGL(init_random_rows, dim3(grid_for(rows * wd)), dim3(256), 0, s, row0, pitch,
+                       rows, gy0, width, wd, seed, density_q32);
+    return hipGetLastError();
+}
+
+hipError_t launch_popcount(const uint32_t *row0, int64_t pitch, int64_t rows, int32_t wd,
+                           unsigned long long *out, hipStream_t s) {
+    hipLaunchKernelGGL(popcount_rows, dim3(grid_for(rows * wd, 256, 4096)), dim3(256), 0, s, row0,
+                       pitch, rows, wd, out);
+    return hipGetLastError();
+}
+
+static void extract_geometry(int64_t width, int32_t &nw, uint32_t &lastmask) {
+    nw = (int32_t)((width + 31) / 32);
+    lastmask = (width & 31) ? ((1u << (width & 31)) - 1u) : 0xffffffffu;
+}
+
+hipError_t launch_extract_count(const uint32_t *a, const uint32_t *b, int64_t pitch,
+                                int64_t rows, int64_t width, uint32_t *row_counts,
+                                unsigned long long *offsets, hipStream_t s) {
+    int32_t nw;
+    uint32_t lastmask;
+    extract_geometry(width, nw, lastmask);
+    const unsigned blocks = grid_for(rows * 64, 256, 16384);
+    hipLaunchKernelGGL(extract_count, dim3(blocks), dim3(256), 0, s, a, b, pitch, rows, nw,
+                       lastmask, row_counts);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(extract_scan, dim3(1), dim3(1024), 0, s, row_counts, rows, offsets);
+    return hipGetLastError();
+}
+
+hipError_t launch_extract_emit(const uint32_t *a, const uint32_t *b, int64_t pitch,
+                               int64_t rows, int64_t width, const unsigned long long *offsets,
+                               int64_t gy0, int32_t *xy, uint64_t cap, hipStream_t s) {
+    int32_t nw;
+    uint32_t lastmask;
+    extract_geometry(width, nw, lastmask);
+    const unsigned blocks = grid_for(rows * 64, 256, 16384);
+    hipLaunchKernelGGL(extract_emit, dim3(blocks), dim3(256), 0, s, a, b, pitch, rows, nw,
+                       lastmask, offsets, gy0, xy, cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_words_out(const uint32_t *row0, int64_t pitch, int64_t rows, int64_t width,
+                            uint64_t *words, hipStream_t s) {
+    const int64_t wpr = width / 64;
+    hipLaunchKernelGGL(words_out, dim3(grid_for(rows * wpr)), dim3(256), 0, s, row0, pitch, rows,
+                       wpr, words);
+    return hipGetLastError();
+}
+
+hipError_t launch_words_in(const uint64_t *words, int64_t rows, int64_t width, int32_t wd,
+                           uint32_t *row0, int64_t pitch, hipStream_t s) {
+    const int64_t wpr = width / 64;
+    hipLaunchKernelGGL(words_in, dim3(grid_for(rows * wd)), dim3(256), 0, s, words, rows, wpr, wd,
+                       row0, pitch);
+    return hipGetLastError();
+}
+
+}  // namespace golhip

@@ -1,0 +1,264 @@
+"""ctypes binding of libgolhip (include/golhip.h) -- the Python side of the drop-in boundary.
+
+This is plumbing: every call goes straight to the C ABI of ``lib/libgolhip.so``, the gfx950
+engine that replaces the reference's ``Broker.Publish`` -> ``GolOP.Work`` path
+(broker/broker.go:157-180, server/server.go:77-107).  There is no CPU fallback: if the
+library or a gfx950 device is missing, calls raise ``GolHipError``.
+
+``import torch`` (when installed) happens before the library is loaded so that one process
+never holds two HIP runtimes: torch's bundled ``libamdhip64.so`` and ``librccl.so`` carry the
+same SONAMEs as /opt/rocm's, so loading torch first makes libgolhip bind to torch's copies.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import numpy as np
+
+try:  # single HIP runtime per process (see module docstring)
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is optional for the binding itself
+    torch = None
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("GOLHIP_LIB", HERE / "lib" / "libgolhip.so"))
+
+OK = 0
+ERR_ARG, ERR_HIP, ERR_OOM, ERR_CAP, ERR_RCCL, ERR_NODEV, ERR_STATE = -1, -2, -3, -4, -5, -6, -7
+NCCL_ID_BYTES = 128
+DENSITY_HALF = 0x80000000
+
+# Every symbol include/golhip.h declares (tests/test_boundary.py checks the .so exports them).
+EXPORTS = [
+    "golhip_version", "golhip_strerror", "golhip_device_count", "golhip_strip_bounds",
+    "golhip_create", "golhip_nccl_unique_id", "golhip_create_rank", "golhip_destroy",
+    "golhip_last_error", "golhip_get_info", "golhip_load_bytes", "golhip_init_random",
+    "golhip_store_bytes", "golhip_store_words", "golhip_load_words", "golhip_step",
+    "golhip_alive_count", "golhip_alive_cells", "golhip_flips", "golhip_turn",
+    "golhip_set_turn", "golhip_set_k", "golhip_set_band_rows", "golhip_sync", "golhip_timing",
+    "golhip_kernel_time",
+]
+
+
+class GolHipError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"golhip error {code}: {msg}")
+        self.code = code
+
+
+class Info(ctypes.Structure):
+    _fields_ = [
+        ("width", ctypes.c_int64), ("height", ctypes.c_int64), ("torus_width", ctypes.c_int64),
+        ("y0", ctypes.c_int64), ("rows", ctypes.c_int64), ("rank", ctypes.c_int32),
+        ("world_size", ctypes.c_int32), ("nshards", ctypes.c_int32), ("k", ctypes.c_int32),
+        ("halo_rows", ctypes.c_int32), ("band_rows", ctypes.c_int32),
+    ]
+
+
+_lib = None
+
+
+def load_library(path: Path | str | None = None) -> ctypes.CDLL:
+    """Load libgolhip.so (raises if it was not built: no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise GolHipError(ERR_NODEV, f"{p} not built (run __graft_entry__.build())")
+    L = ctypes.CDLL(str(p))
+    H = ctypes.c_void_p
+    i64, i32, u64p = ctypes.c_int64, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)
+    i64p = ctypes.POINTER(ctypes.c_int64)
+    sig = {
+        "golhip_version": ([], i32),
+        "golhip_strerror": ([i32], ctypes.c_char_p),
+        "golhip_device_count": ([ctypes.POINTER(i32)], i32),
+        "golhip_strip_bounds": ([i64, i32, i32, i64p, i64p], i32),
+        "golhip_create": ([i32, i32, i32, i32, ctypes.POINTER(H)], i32),
+        "golhip_nccl_unique_id": ([ctypes.c_char_p], i32),
+        "golhip_create_rank": ([i32, i32, i32, i32, i32, i32, ctypes.c_char_p, ctypes.POINTER(H)], i32),
+        "golhip_destroy": ([H], i32),
+        "golhip_last_error": ([H], ctypes.c_char_p),
+        "golhip_get_info": ([H, ctypes.POINTER(Info)], i32),
+        "golhip_load_bytes": ([H, ctypes.c_void_p, ctypes.c_size_t], i32),
+        "golhip_init_random": ([H, ctypes.c_uint64, ctypes.c_uint32], i32),
+        "golhip_store_bytes": ([H, ctypes.c_void_p, ctypes.c_size_t], i32),
+        "golhip_store_words": ([H, ctypes.c_void_p], i32),
+        "golhip_load_words": ([H, ctypes.c_void_p], i32),
+        "golhip_step": ([H, i64, ctypes.c_void_p], i32),
+        "golhip_alive_count": ([H, u64p], i32),
+        "golhip_alive_cells": ([H, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)], i32),
+        "golhip_flips": ([H, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)], i32),
+        "golhip_turn": ([H, i64p], i32),
+        "golhip_set_turn": ([H, i64], i32),
+        "golhip_set_k": ([H, i32], i32),
+        "golhip_set_band_rows": ([H, i32], i32),
+        "golhip_sync": ([H], i32),
+        "golhip_timing": ([H, i32], i32),
+        "golhip_kernel_time": ([H, ctypes.POINTER(ctypes.c_double), i64p, i64p], i32),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    load_library().golhip_device_count(ctypes.byref(n))
+    return n.value
+
+
+def strip_bounds(height: int, world_size: int, rank: int) -> tuple[int, int]:
+    """Rows [y0, y0+rows) of `rank` (pure host arithmetic, no device)."""
+    y0, rows = ctypes.c_int64(), ctypes.c_int64()
+    rc = load_library().golhip_strip_bounds(height, world_size, rank, ctypes.byref(y0), ctypes.byref(rows))
+    if rc != OK:
+        raise GolHipError(rc, "strip_bounds: invalid arguments")
+    return y0.value, rows.value
+
+
+def nccl_unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(NCCL_ID_BYTES)
+    rc = load_library().golhip_nccl_unique_id(buf)
+    if rc != OK:
+        raise GolHipError(rc, "ncclGetUniqueId failed")
+    return buf.raw
+
+
+class Engine:
+    """One libgolhip handle.  Mirrors the broker's role: the board lives on the GPU(s)."""
+
+    def __init__(self, width: int, height: int, ngpus: int = 1, k: int = 1, *, rank: int | None = None,
+                 world_size: int = 1, device: int = 0, nccl_id: bytes | None = None):
+        L = load_library()
+        self._L = L
+        self._h = ctypes.c_void_p()
+        if rank is None:
+            rc = L.golhip_create(width, height, ngpus, k, ctypes.byref(self._h))
+        else:
+            rc = L.golhip_create_rank(width, height, rank, world_size, device, k, nccl_id,
+                                      ctypes.byref(self._h))
+        if rc != OK:
+            raise GolHipError(rc, L.golhip_strerror(rc).decode())
+        self.info = self.get_info()
+
+    # -- plumbing
+    def _check(self, rc: int) -> int:
+        if rc != OK:
+            raise GolHipError(rc, self._L.golhip_last_error(self._h).decode() or
+                              self._L.golhip_strerror(rc).decode())
+        return rc
+
+    def close(self):
+        if self._h:
+            self._L.golhip_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def get_info(self) -> Info:
+        info = Info()
+        self._check(self._L.golhip_get_info(self._h, ctypes.byref(info)))
+        return info
+
+    # -- board in/out
+    def load(self, cells: np.ndarray):
+        cells = np.ascontiguousarray(cells, dtype=np.uint8)
+        assert cells.shape == (self.info.rows, self.info.width), cells.shape
+        self._check(self._L.golhip_load_bytes(self._h, cells.ctypes.data, cells.strides[0]))
+
+    def init_random(self, seed: int, density_q32: int = DENSITY_HALF):
+        self._check(self._L.golhip_init_random(self._h, seed, density_q32))
+
+    def store(self) -> np.ndarray:
+        out = np.empty((self.info.rows, self.info.width), dtype=np.uint8)
+        self._check(self._L.golhip_store_bytes(self._h, out.ctypes.data, out.strides[0]))
+        return out
+
+    def store_words(self) -> np.ndarray:
+        out = np.empty((self.info.rows, self.info.width // 64), dtype=np.uint64)
+        self._check(self._L.golhip_store_words(self._h, out.ctypes.data))
+        return out
+
+    def load_words(self, words: np.ndarray):
+        words = np.ascontiguousarray(words, dtype=np.uint64)
+        assert words.shape == (self.info.rows, self.info.width // 64)
+        self._check(self._L.golhip_load_words(self._h, words.ctypes.data))
+
+    # -- hot path
+    def step(self, turns: int, counts: bool = False) -> np.ndarray | None:
+        if counts:
+            out = np.zeros(max(turns, 1), dtype=np.uint64)
+            self._check(self._L.golhip_step(self._h, turns, out.ctypes.data))
+            return out[:turns]
+        self._check(self._L.golhip_step(self._h, turns, None))
+        return None
+
+    def alive_count(self) -> int:
+        v = ctypes.c_uint64()
+        self._check(self._L.golhip_alive_count(self._h, ctypes.byref(v)))
+        return v.value
+
+    def _cells(self, fn) -> np.ndarray:
+        n = ctypes.c_size_t(0)
+        rc = fn(self._h, None, 0, ctypes.byref(n))
+        if rc not in (OK, ERR_CAP):
+            self._check(rc)
+        out = np.empty((max(n.value, 1), 2), dtype=np.int32)
+        self._check(fn(self._h, out.ctypes.data, n.value, ctypes.byref(n)))
+        return out[: n.value]
+
+    def alive_cells(self) -> np.ndarray:
+        """(n, 2) int32 array of (x, y), row-major (gol/distributor.go:153-166)."""
+        return self._cells(self._L.golhip_alive_cells)
+
+    def flips(self) -> np.ndarray:
+        """(n, 2) int32 array of (x, y) that changed in the last generation."""
+        return self._cells(self._L.golhip_flips)
+
+    @property
+    def turn(self) -> int:
+        t = ctypes.c_int64()
+        self._check(self._L.golhip_turn(self._h, ctypes.byref(t)))
+        return t.value
+
+    @turn.setter
+    def turn(self, value: int):
+        self._check(self._L.golhip_set_turn(self._h, value))
+
+    # -- tuning / measurement
+    def set_k(self, k: int):
+        self._check(self._L.golhip_set_k(self._h, k))
+        self.info = self.get_info()
+
+    def set_band_rows(self, rows: int):
+        self._check(self._L.golhip_set_band_rows(self._h, rows))
+        self.info = self.get_info()
+
+    def sync(self):
+        self._check(self._L.golhip_sync(self._h))
+
+    def timing(self, enable: bool):
+        self._check(self._L.golhip_timing(self._h, int(enable)))
+
+    def kernel_time(self) -> tuple[float, int, int]:
+        ms, launches, gens = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()
+        self._check(self._L.golhip_kernel_time(self._h, ctypes.byref(ms), ctypes.byref(launches),
+                                               ctypes.byref(gens)))
+        return ms.value, launches.value, gens.value

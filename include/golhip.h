@@ -1,0 +1,132 @@
+/*
+ * golhip.h -- C ABI of libgolhip, the MI355X (gfx950) Game-of-Life engine.
+ *
+ * libgolhip replaces the reference's per-turn compute path (Oliver-Cairns/distributed-gol):
+ *
+ *   reference (Go, net/rpc)                                   replaced by
+ *   -------------------------------------------------------   ----------------------------------
+ *   Broker.Publish(req, res)        broker/broker.go:157-180  golhip_step()  (res.World = next gen)
+ *     publish: 4-strip fan-out      broker/broker.go:37-56    row strips over GPUs (golhip_create*)
+ *     strip stitch + worldSave      broker/broker.go:168-175  device-resident board, halos by RCCL
+ *   GolOP.Work(req, res)            server/server.go:77-107   gfx950 stencil kernel (k gens/launch)
+ *     calculateNextState/updateCell server/server.go:21-75    bit-sliced B3/S23 (64 cells per uint64)
+ *   calculateAliveCells             gol/distributor.go:153-166 golhip_alive_count / golhip_alive_cells
+ *   CellFlipped diff                gol/distributor.go:53-59  golhip_flips
+ *   readPgmImage / writePgmImage    gol/io.go:42-128          golhip_load_bytes / golhip_store_bytes
+ *   Broker.CheckStates/Pause state  broker/broker.go:124-155  golhip_turn + the resident board
+ *
+ * Conventions (all functions):
+ *   - return 0 (GOLHIP_OK) or a negative GOLHIP_ERR_* code; golhip_last_error(h) describes the
+ *     last failure on that handle (the reference only prints RPC errors, gol/distributor.go:50-52;
+ *     here every failure is reported, never silently ignored).
+ *   - a handle is owned by ONE host thread; caller-owned host buffers are never retained.
+ *   - cells are bytes: 0 = dead, any nonzero = alive on input (gol_test.go:119), 255 on output
+ *     (server/server.go:37,46).  The board is a torus (server/server.go:58-69).
+ *   - "the handle's rows" are [y0, y0+rows) of the global board (golhip_get_info): the whole board
+ *     for golhip_create(), this rank's row strip for golhip_create_rank().
+ *   - functions marked COLLECTIVE must be called by every rank of a golhip_create_rank() group.
+ */
+#ifndef GOLHIP_H
+#define GOLHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct golhip_engine *golhip_t;
+
+#define GOLHIP_OK 0
+#define GOLHIP_ERR_ARG (-1)   /* invalid argument (sizes, null pointers, k range) */
+#define GOLHIP_ERR_HIP (-2)   /* HIP runtime error */
+#define GOLHIP_ERR_OOM (-3)   /* device allocation failed */
+#define GOLHIP_ERR_CAP (-4)   /* output capacity too small: *n holds the required count */
+#define GOLHIP_ERR_RCCL (-5)  /* RCCL error */
+#define GOLHIP_ERR_NODEV (-6) /* no gfx950 device / not enough devices */
+#define GOLHIP_ERR_STATE (-7) /* call not valid in the current state (e.g. flips after k>1) */
+
+#define GOLHIP_NCCL_ID_BYTES 128
+#define GOLHIP_DENSITY_HALF 0x80000000u /* density_q32 for p = 0.5 (raw random bits) */
+
+typedef struct {
+    int64_t width;        /* logical board width  (Params.ImageWidth,  gol/gol.go:6-11) */
+    int64_t height;       /* logical board height (Params.ImageHeight) */
+    int64_t torus_width;  /* device torus width L = lcm(width, 128) (horizontal replication) */
+    int64_t y0;           /* first global row held by this handle */
+    int64_t rows;         /* rows held by this handle */
+    int32_t rank;         /* first rank of this handle */
+    int32_t world_size;   /* number of row strips (GPUs) the board is split over */
+    int32_t nshards;      /* strips owned by this handle (ngpus for golhip_create) */
+    int32_t k;            /* generations per stencil launch (temporal blocking depth) */
+    int32_t halo_rows;    /* halo rows allocated per strip edge (>= k when world_size > 1) */
+    int32_t band_rows;    /* rows per wave band in the stencil launch (0 = automatic) */
+} golhip_info;
+
+/* ---- library / devices ------------------------------------------------------------------ */
+int golhip_version(void);                 /* e.g. 100 for 0.1.0 */
+const char *golhip_strerror(int code);
+int golhip_device_count(int *out);        /* visible HIP devices */
+/* Pure host helper: the row strip of `rank` when `height` rows are split over world_size GPUs. */
+int golhip_strip_bounds(int64_t height, int world_size, int rank, int64_t *y0, int64_t *rows);
+
+/* ---- lifetime --------------------------------------------------------------------------- */
+/* One process, `ngpus` devices (0..ngpus-1), row strips with RCCL halo exchange between them
+ * (the on-node replacement of the broker + 4 servers, broker/broker.go:191-205). k = max
+ * generations per stencil launch (1..32). */
+int golhip_create(int width, int height, int ngpus, int k, golhip_t *out);
+/* One process per GPU: rank `rank` of `world_size`, on HIP device `device`. nccl_id: the
+ * GOLHIP_NCCL_ID_BYTES produced by golhip_nccl_unique_id() on rank 0 (NULL if world_size == 1). */
+int golhip_nccl_unique_id(uint8_t *out /* GOLHIP_NCCL_ID_BYTES */);
+int golhip_create_rank(int width, int height, int rank, int world_size, int device, int k,
+                       const uint8_t *nccl_id, golhip_t *out);
+int golhip_destroy(golhip_t h);
+const char *golhip_last_error(golhip_t h);
+int golhip_get_info(golhip_t h, golhip_info *out);
+
+/* ---- board in / out (gol/io.go:42-128, util/cell.go) ------------------------------------- */
+/* Load the handle's rows from 0/nonzero bytes (row y at cells + (y - y0) * row_stride). */
+int golhip_load_bytes(golhip_t h, const uint8_t *cells, size_t row_stride);
+/* Counter-based random board, regenerated on device (identical for any world_size):
+ * width % 64 == 0; logical uint64 word i = y * width/64 + j:
+ *   density_q32 == GOLHIP_DENSITY_HALF : word = splitmix64(seed + (i+1) * 0x9E3779B97F4A7C15)
+ *   otherwise : cell c = y*width + x alive iff (uint32)splitmix64(seed + (c+1)*0x9E37..) < density_q32 */
+int golhip_init_random(golhip_t h, uint64_t seed, uint32_t density_q32);
+/* Store the handle's rows as 0/255 bytes (the PGM body, gol/io.go:76-81). */
+int golhip_store_bytes(golhip_t h, uint8_t *out, size_t row_stride);
+/* Packed little-endian uint64 rows of the handle's rows (width % 64 == 0): rows * width/64 words. */
+int golhip_store_words(golhip_t h, uint64_t *out);
+int golhip_load_words(golhip_t h, const uint64_t *in);
+
+/* ---- the hot path ------------------------------------------------------------------------ */
+/* Advance `turns` generations (Broker.Publish called `turns` times, gol/distributor.go:48-49).
+ * alive_per_turn (nullable, len turns): alive cells after each completed turn, counted inside the
+ * stencil launch (the AliveCellsCount/TurnComplete source, gol/distributor.go:168-191).
+ * COLLECTIVE when alive_per_turn != NULL or world_size > 1.  Asynchronous when alive_per_turn
+ * is NULL (use golhip_sync to wait). */
+int golhip_step(golhip_t h, int64_t turns, uint64_t *alive_per_turn);
+/* Alive cells of the whole board (COLLECTIVE: sums over ranks). */
+int golhip_alive_count(golhip_t h, uint64_t *out);
+/* Alive cells of the handle's rows as (x, y) int32 pairs, row-major (gol/distributor.go:153-166).
+ * If the count exceeds cap, returns GOLHIP_ERR_CAP with *n = required count. */
+int golhip_alive_cells(golhip_t h, int32_t *xy, size_t cap, size_t *n);
+/* Cells that changed in the last generation (valid after a step whose last launch advanced 1
+ * generation; gol/distributor.go:53-59), (x, y) pairs, row-major; GOLHIP_ERR_STATE otherwise. */
+int golhip_flips(golhip_t h, int32_t *xy, size_t cap, size_t *n);
+/* Completed turns since the last load (the broker's `turn`, broker/broker.go:140). */
+int golhip_turn(golhip_t h, int64_t *out);
+int golhip_set_turn(golhip_t h, int64_t turn);
+
+/* ---- tuning / measurement ---------------------------------------------------------------- */
+int golhip_set_k(golhip_t h, int k);                 /* 1..32, <= halo_rows when world_size > 1 */
+int golhip_set_band_rows(golhip_t h, int band_rows); /* 0 = automatic */
+int golhip_sync(golhip_t h);                         /* wait for all queued device work */
+/* Per-launch HIP-event timing of the stencil kernel on the handle's first strip. */
+int golhip_timing(golhip_t h, int enable);
+int golhip_kernel_time(golhip_t h, double *total_ms, int64_t *launches, int64_t *generations);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GOLHIP_H */

@@ -1,0 +1,121 @@
+"""GPU parity: libgolhip (through its C ABI) against the oracle and the reference's fixtures.
+
+Bit-exact for every board, count and cell list (integer/byte work: no tolerance).
+"""
+import numpy as np
+import pytest
+
+from conftest import REF
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [16, 64, 512]
+KS = [1, 2, 4, 8, 16, 32]
+
+
+def run_engine(golhip, board, turns, k=1, counts=False, band_rows=0):
+    h, w = board.shape
+    with golhip.Engine(w, h, k=k) as e:
+        if band_rows:
+            e.set_band_rows(band_rows)
+        e.load(board)
+        c = e.step(turns, counts=counts)
+        return e.store(), c, e.alive_cells(), e.alive_count()
+
+
+@pytest.mark.parametrize("n", SIZES)
+@pytest.mark.parametrize("turns", [0, 1, 100])
+def test_check_images(golhip, oracle, n, turns):
+    """TestGol / TestPgm (gol_test.go:15-47, pgm_test.go:10-42): final board == check image."""
+    _, _, board = oracle.read_pgm(REF / f"images/{n}x{n}.pgm")
+    expected_pgm = (REF / f"check/images/{n}x{n}x{turns}.pgm").read_bytes()
+    _, _, expected = oracle.read_pgm(REF / f"check/images/{n}x{n}x{turns}.pgm")
+    for k in (1, 8, 32):
+        out, _, cells, count = run_engine(golhip, board, turns, k=k)
+        assert oracle.pgm_bytes(out) == expected_pgm, (n, turns, k)
+        exp_cells = oracle.alive_cells(expected)
+        assert [tuple(c) for c in cells.tolist()] == exp_cells
+        assert count == len(exp_cells)
+
+
+@pytest.mark.parametrize("n", SIZES)
+@pytest.mark.parametrize("k", [1, 8, 16])
+def test_alive_csv_every_turn(golhip, oracle, n, k):
+    """check/alive/NxN.csv: the count after every one of 10000 turns (count_test.go, sdl_test.go)."""
+    _, _, board = oracle.read_pgm(REF / f"images/{n}x{n}.pgm")
+    expected = oracle.read_alive_csv(REF / f"check/alive/{n}x{n}.csv")
+    _, counts, _, _ = run_engine(golhip, board, 10000, k=k, counts=True)
+    assert [int(c) for c in counts] == [expected[t] for t in range(1, 10001)]
+
+
+@pytest.mark.parametrize("shape", [(128, 128), (96, 200), (300, 128), (1000, 640), (257, 4096),
+                                   (2048, 2048), (40, 8192), (33, 12800)])
+@pytest.mark.parametrize("k", KS)
+def test_random_boards_vs_oracle(golhip, oracle, shape, k):
+    h, w = shape
+    rng = np.random.default_rng(h * 7919 + w)
+    board = ((rng.random(shape) < 0.45) * 255).astype(np.uint8)
+    turns = 2 * k + 3
+    exp, exp_counts = oracle.packed_run(board, turns)
+    for band in (0, 5, 64):
+        out, counts, _, _ = run_engine(golhip, board, turns, k=k, counts=True, band_rows=band)
+        assert np.array_equal(out, exp), (shape, k, band)
+        assert np.array_equal(counts.astype(np.int64), exp_counts), (shape, k, band)
+
+
+def test_flips_match_oracle(golhip, oracle):
+    """CellFlipped per turn (gol/distributor.go:53-59) from the XOR + compaction kernels."""
+    _, _, board = oracle.read_pgm(REF / "images/512x512.pgm")
+    with golhip.Engine(512, 512, k=8) as e:
+        e.load(board)
+        prev = board.copy()
+        for t in range(20):
+            e.step(1)
+            cur = e.store()
+            got = [tuple(c) for c in e.flips().tolist()]
+            assert got == oracle.flips(prev, cur)
+            prev = cur
+        e.step(8)
+        with pytest.raises(golhip.GolHipError):
+            e.flips()
+
+
+def test_init_random_matches_oracle(golhip, oracle):
+    for (w, h, seed, dens) in [(128, 64, 2, golhip.DENSITY_HALF), (192, 50, 3, 1 << 30),
+                               (5120, 16, 2, golhip.DENSITY_HALF)]:
+        with golhip.Engine(w, h) as e:
+            e.init_random(seed, dens)
+            assert np.array_equal(e.store_words(), oracle.init_random(w, h, seed, dens))
+
+
+def test_words_roundtrip_and_steps(golhip, oracle):
+    w, h = 5120, 96
+    words = oracle.init_random(w, h, seed=5)
+    with golhip.Engine(w, h, k=4) as e:
+        e.load_words(words)
+        assert np.array_equal(e.store_words(), words)
+        counts = e.step(9, counts=True)
+        ref = words.copy()
+        ref_counts = oracle.packed_run_words(ref, 9)
+        assert np.array_equal(e.store_words(), ref)
+        assert np.array_equal(counts.astype(np.int64), ref_counts)
+
+
+def test_turn_counter(golhip):
+    with golhip.Engine(128, 128, k=8) as e:
+        e.init_random(1)
+        e.step(13)
+        assert e.turn == 13
+        e.turn = 100
+        assert e.turn == 100
+
+
+def test_cap_error_reports_required_count(golhip, oracle):
+    _, _, board = oracle.read_pgm(REF / "images/64x64.pgm")
+    with golhip.Engine(64, 64) as e:
+        e.load(board)
+        import ctypes
+        n = ctypes.c_size_t(0)
+        buf = np.empty((10, 2), np.int32)
+        rc = e._L.golhip_alive_cells(e._h, buf.ctypes.data, 10, ctypes.byref(n))
+        assert rc == golhip.ERR_CAP and n.value == 2819
