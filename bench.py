@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""Benchmark of the hot path: GCUPS and % of the HBM roofline of the gfx950 stencil.
+
+A "step" is one generation (turn) of the whole board: one Broker.Publish -> 4x GolOP.Work round
+of the reference (broker/broker.go:157-180, server/server.go:77-107).
+
+Workload (BASELINE.json configs[2], the metric's "65536^2 @1 GPU"): a 65536 x 65536 random
+board (p = 0.5, seed 3) per GPU.  With --gpus N (one process per GPU, launched by
+torch.distributed.run) the board is 65536 wide and 65536*N tall, split into N row strips with
+k-row RCCL halo exchange over xGMI (weak scaling: per-GPU work fixed).  --size/--height select
+other boards (e.g. --size 262144 for configs[3], strong scaling).
+
+Prints ONE JSON line on rank 0 (keys per the driver contract), plus:
+  roofline     : algorithmic bytes (0.25 B per cell-update) per stencil launch / the launch's
+                 average duration from HIP events recorded on the engine's compute stream;
+  cpu_baseline : the reference algorithm (oracle/ port of server/server.go + broker split,
+                 byte per cell, 4 servers x T threads) timed on this host on a bounded sample;
+  k_sweep      : GCUPS per temporal-blocking depth k (N == 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "distributed-gol_amd"))
+
+import torch  # noqa: E402  (first: one HIP runtime per process, see golhip.py)
+import torch.distributed as dist  # noqa: E402
+
+import golhip  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+BYTES_PER_CELL_UPDATE = 0.25  # 1 packed bit read + 1 packed bit written per cell per generation
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=256, help="timed generations")
+    ap.add_argument("--warmup", type=int, default=32, help="untimed generations")
+    ap.add_argument("--size", type=int, default=65536, help="board width")
+    ap.add_argument("--height", type=int, default=0,
+                    help="total board height (default: size * N, weak scaling)")
+    ap.add_argument("--k", type=int, default=8, help="generations per stencil launch")
+    ap.add_argument("--band-rows", type=int, default=0)
+    ap.add_argument("--seed", type=int, default=3)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-sweep", action="store_true", help="skip the k sweep")
+    ap.add_argument("--cpu-size", type=int, default=16384)
+    ap.add_argument("--cpu-turns", type=int, default=24)
+    ap.add_argument("--pmc-file", default=str(ROOT / "profiles" / "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def timed_steps(eng: golhip.Engine, steps: int, world: int) -> float:
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    eng.sync()
+    t0 = time.perf_counter()
+    eng.step(steps)
+    eng.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt
+
+
+def cpu_baseline(size: int, turns: int, threads_per_server: int) -> dict:
+    """The reference's algorithm (oracle/gol_oracle.c oracle_ref_*), timed on this host."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import numpy as np
+
+    import oracle
+
+    board = oracle.unpack(oracle.init_random(size, size, seed=3), size)
+    t0 = time.perf_counter()
+    oracle.ref_run(board, turns, threads=threads_per_server, servers=4, fanout_copy=False)
+    dt = time.perf_counter() - t0
+    cups = size * size * turns / dt
+    del board, np
+    return {
+        "value": round(cups / 1e9, 4),
+        "unit": "GCUPS",
+        "cores": 4 * threads_per_server,
+        "kind": "port",
+        "sample": (f"{size}x{size} random p=0.5 seed 3, {turns} turns of the reference algorithm "
+                   f"(byte cells, branchy torus wrap + /255, fresh rows per turn, 4 broker strips x "
+                   f"{threads_per_server} goroutine-threads = {4 * threads_per_server} OS threads); "
+                   f"gob/TCP fan-out excluded; {dt:.1f} s"),
+    }
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local)
+
+    width = a.size
+    height = a.height or a.size * world
+    nccl_id = None
+    if world > 1:
+        obj = [golhip.nccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        nccl_id = obj[0]
+    eng = golhip.Engine(width, height, k=a.k, rank=rank, world_size=world, device=local,
+                        nccl_id=nccl_id)
+    if a.band_rows:
+        eng.set_band_rows(a.band_rows)
+    eng.init_random(a.seed)
+    local_cells = eng.info.rows * width
+
+    eng.step(a.warmup)
+    eng.sync()
+
+    # timed region: exactly a.steps generations, per-launch HIP events on the compute stream
+    eng.timing(True)
+    dt = timed_steps(eng, a.steps, world)
+    kern_ms, launches, gens = eng.kernel_time()
+    eng.timing(False)
+
+    total_updates = width * height * a.steps
+    gcups = total_updates / dt / 1e9
+    ms_per_step = dt * 1e3 / a.steps
+
+    # roofline of the dominant kernel (gol_stencil<k>) on this rank
+    avg_launch_ms = kern_ms / max(launches, 1)
+    gens_per_launch = gens / max(launches, 1)
+    alg_bytes_per_launch = BYTES_PER_CELL_UPDATE * local_cells * gens_per_launch
+    achieved = alg_bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
+    traffic = None
+    try:
+        pmc = json.loads(Path(a.pmc_file).read_text())
+        key = f"{width}x{eng.info.rows}_k{a.k}"
+        if key in pmc:
+            traffic = pmc[key]["hbm_bytes_per_launch"]
+    except Exception:
+        pass
+
+    sweep = None
+    if world == 1 and not a.no_sweep:
+        sweep = {}
+        for kk in (1, 2, 4, 8, 16, 32):
+            eng.set_k(kk)
+            eng.step(2 * kk)
+            n = max(4 * kk, 32)
+            t = timed_steps(eng, n, 1)
+            sweep[str(kk)] = round(width * height * n / t / 1e9, 1)
+        eng.set_k(a.k)
+
+    checksum = eng.alive_count()  # collective
+    eng.close()
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu:
+        cpu = cpu_baseline(a.cpu_size, a.cpu_turns, threads_per_server=4)
+
+    if rank == 0:
+        line = {
+            "metric": "cell-updates/sec (GCUPS)",
+            "value": round(gcups, 2),
+            "unit": "GCUPS",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak" if not a.height else "strong",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (counter-based splitmix64 random board, p=0.5, generated on device)",
+            "config": {
+                "workload": (f"{width}x{height} torus, random p=0.5 seed {a.seed}, "
+                             f"{world} row strip(s) of {eng.info.rows} rows, k={a.k} gens/launch"),
+                "width": width, "height": height, "k": a.k, "parallelism": f"rows{world}",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel": f"gol_stencil<{a.k}>",
+                "avg_launch_us": round(avg_launch_ms * 1e3, 2),
+                "gens_per_launch": gens_per_launch,
+            },
+            "cpu_baseline": cpu,
+            "k_sweep_gcups": sweep,
+            "alive_after": int(checksum),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
