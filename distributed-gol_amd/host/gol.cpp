@@ -1,0 +1,323 @@
+// gol.cpp -- the controller ("distributor") of the host mirror, driving libgolhip.
+//
+// Reference flow (gol/distributor.go:194-263) and what replaces each part here:
+//   read images/WxH.pgm, CellFlipped for initially alive cells  :204-216  -> same
+//   rpc.Dial(broker) + makeCall/CheckStates resume              :218,69-91 -> Engine (+ saved
+//                                                                             state of 'q')
+//   Call(): per turn Broker.Publish, O(N^2) diff -> CellFlipped :45-67     -> golhip_step(1) +
+//                                                                             golhip_flips, or
+//                                                                             chunked
+//                                                                             golhip_step(n)
+//   countAliveCells: O(N^2) scan per turn, 2 s ticker           :168-191   -> per-turn counts
+//                                                                             from the stencil
+//   manageKeyPresses s/q/p/k                                    :105-151   -> serviced between
+//                                                                             chunks
+//   FinalTurnComplete, out/WxHxT.pgm, StateChange Quitting      :235-262   -> same
+//
+// Deliberate deviations from reference quirks, documented in
+// FinalTurnComplete/StateChange carry the real completed-turn count (the reference
+// always sends 0); the 's' snapshot is named with the completed turn; a tick before the first
+// completed turn reports the initial count; 'q' and 'k' end Run() (closing `events`) instead of
+// leaving the turn loop running.
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <map>
+#include <mutex>
+#include <thread>
+
+#include "engine.hpp"
+#include "gol.hpp"
+
+namespace gol {
+
+std::string to_string(State s) {
+    switch (s) {
+        case State::Paused: return "Paused";
+        case State::Executing: return "Executing";
+        case State::Quitting: return "Quitting";
+    }
+    return "Incorrect State";
+}
+
+std::string Event::String() const {
+    char buf[128];
+    switch (kind) {
+        case EventKind::AliveCellsCount:
+            std::snprintf(buf, sizeof buf, "Alive Cells %lld", (long long)CellsCount);
+            return buf;
+        case EventKind::ImageOutputComplete: return "File " + Filename + " output complete";
+        case EventKind::StateChange: return to_string(NewState);
+        default: return "";
+    }
+}
+
+Event Event::alive_cells_count(int t, int64_t n) {
+    Event e;
+    e.kind = EventKind::AliveCellsCount;
+    e.CompletedTurns = t;
+    e.CellsCount = n;
+    return e;
+}
+Event Event::image_output_complete(int t, std::string f) {
+    Event e;
+    e.kind = EventKind::ImageOutputComplete;
+    e.CompletedTurns = t;
+    e.Filename = std::move(f);
+    return e;
+}
+Event Event::state_change(int t, State s) {
+    Event e;
+    e.kind = EventKind::StateChange;
+    e.CompletedTurns = t;
+    e.NewState = s;
+    return e;
+}
+Event Event::cell_flipped(int t, Cell c) {
+    Event e;
+    e.kind = EventKind::CellFlipped;
+    e.CompletedTurns = t;
+    e.cell = c;
+    return e;
+}
+Event Event::turn_complete(int t) {
+    Event e;
+    e.kind = EventKind::TurnComplete;
+    e.CompletedTurns = t;
+    return e;
+}
+Event Event::final_turn_complete(int t, std::vector<Cell> alive) {
+    Event e;
+    e.kind = EventKind::FinalTurnComplete;
+    e.CompletedTurns = t;
+    e.Alive = std::make_shared<std::vector<Cell>>(std::move(alive));
+    return e;
+}
+
+namespace {
+
+// The broker's pause state (broker/broker.go:33-35 worldSave/turn/size), kept device-resident:
+// 'q' parks the engine here; the next Run() of the same size resumes from it (CheckStates).
+struct Saved {
+    std::unique_ptr<Engine> engine;
+    int width = 0, height = 0;
+    int turn = 0;
+};
+std::mutex g_saved_mu;
+Saved g_saved;
+
+std::vector<Cell> to_cells(const std::vector<int32_t> &xy) {
+    std::vector<Cell> out(xy.size() / 2);
+    for (size_t i = 0; i < out.size(); ++i) out[i] = {xy[2 * i], xy[2 * i + 1]};
+    return out;
+}
+
+struct Ticker {  // gol/distributor.go:168-191 with the 2 s time.Ticker of :228
+    std::mutex mu;
+    int turn = 0;
+    int64_t count = 0;
+    std::atomic<bool> stop{false};
+    std::thread th;
+
+    void start(Channel<Event> *events, int period_ms) {
+        th = std::thread([this, events, period_ms] {
+            auto next = std::chrono::steady_clock::now() + std::chrono::milliseconds(period_ms);
+            while (!stop.load()) {
+                std::this_thread::sleep_for(std::chrono::milliseconds(5));
+                if (std::chrono::steady_clock::now() < next) continue;
+                next += std::chrono::milliseconds(period_ms);
+                int t;
+                int64_t c;
+                {
+                    std::lock_guard<std::mutex> lk(mu);
+                    t = turn;
+                    c = count;
+                }
+                try {
+                    events->send(Event::alive_cells_count(t, c));
+                } catch (...) {
+                    return;  // events closed
+                }
+            }
+        });
+    }
+    void update(int t, int64_t c) {
+        std::lock_guard<std::mutex> lk(mu);
+        turn = t;
+        count = c;
+    }
+    void halt() {
+        stop = true;
+        if (th.joinable()) th.join();
+    }
+};
+
+std::string board_name(const Params &p) {
+    return std::to_string(p.ImageWidth) + "x" + std::to_string(p.ImageHeight);
+}
+
+void snapshot(Engine &eng, const Params &p, const RunOptions &o, const std::string &name) {
+    Image img{p.ImageWidth, p.ImageHeight, eng.store()};
+    write_pgm(o.out_dir + "/" + name + ".pgm", img);
+}
+
+}  // namespace
+
+void reset_saved_state() {
+    std::lock_guard<std::mutex> lk(g_saved_mu);
+    g_saved = Saved{};
+}
+
+void Run(Params p, Channel<Event> *events, Channel<char> *keyPresses, const RunOptions &o) {
+    const std::string name = board_name(p);
+    Image img = read_pgm(o.image_dir + "/" + name + ".pgm");
+    if (img.width != p.ImageWidth) throw std::runtime_error("Incorrect width");
+    if (img.height != p.ImageHeight) throw std::runtime_error("Incorrect height");
+
+    int turn = 0;
+    const std::vector<Cell> initial = alive_cells_of(img);
+    if (o.flip_events)  // gol/distributor.go:212-214
+        for (const Cell &c : initial) events->send(Event::cell_flipped(0, c));
+
+    // makeCall: resume a board parked by 'q' when the size matches (gol/distributor.go:69-91,
+    // broker/broker.go:124-141); CheckStates clears the saved state either way.
+    std::unique_ptr<Engine> eng;
+    if (p.Turns > 0) {
+        std::lock_guard<std::mutex> lk(g_saved_mu);
+        if (g_saved.engine && g_saved.width == p.ImageWidth && g_saved.height == p.ImageHeight) {
+            eng = std::move(g_saved.engine);
+            turn = g_saved.turn;
+        }
+        g_saved = Saved{};
+    }
+    if (!eng) {
+        eng = std::make_unique<Engine>(p.ImageWidth, p.ImageHeight, o.ngpus, o.k);
+        for (auto &px : img.pixels) px = px ? 255 : 0;
+        eng->load(img.pixels);
+    }
+    eng->set_turn(turn);
+
+    Ticker ticker;
+    ticker.update(turn, turn == 0 ? (int64_t)initial.size() : (int64_t)eng->alive_count());
+    ticker.start(events, o.ticker_ms);
+
+    bool quit = false;
+    // Keys (gol/distributor.go:115-148), serviced between step chunks.
+    auto handle_key = [&](char key, bool &paused) {
+        switch (key) {
+            case 's': {
+                const std::string f = name + "x" + std::to_string(turn);
+                snapshot(*eng, p, o, f);
+                events->send(Event::image_output_complete(turn, f));
+                break;
+            }
+            case 'q': {
+                events->send(Event::state_change(turn, State::Quitting));
+                {
+                    std::lock_guard<std::mutex> lk(g_saved_mu);
+                    g_saved.engine = std::move(eng);
+                    g_saved.width = p.ImageWidth;
+                    g_saved.height = p.ImageHeight;
+                    g_saved.turn = turn;
+                }
+                quit = true;
+                break;
+            }
+            case 'k': {
+                const std::string f = name + "x" + std::to_string(turn);
+                snapshot(*eng, p, o, f);
+                events->send(Event::image_output_complete(turn, f));
+                events->send(Event::state_change(turn, State::Quitting));
+                eng.reset();  // Broker.Quit -> GolOP.Quit: the workers go away
+                reset_saved_state();
+                quit = true;
+                break;
+            }
+            case 'p':
+                paused = !paused;
+                events->send(Event::state_change(turn, paused ? State::Paused : State::Executing));
+                break;
+            default: break;
+        }
+    };
+
+    const int W = p.ImageWidth, H = p.ImageHeight;
+    (void)W;
+    (void)H;
+    int64_t chunk = 1;
+    bool paused = false;
+    while (!quit && turn < p.Turns) {
+        if (keyPresses) {
+            while (!quit) {
+                std::optional<char> key = paused ? keyPresses->recv() : keyPresses->try_recv();
+                if (!key) break;
+                handle_key(*key, paused);
+                if (!paused) break;
+            }
+        }
+        if (quit) break;
+        if (o.flip_events) {
+            // one turn: step, diff -> CellFlipped{turn}, TurnComplete{turn+1}
+            const std::vector<uint64_t> c = eng->step(1, true);
+            for (const Cell &cell : to_cells(eng->flips()))
+                events->send(Event::cell_flipped(turn, cell));
+            ++turn;
+            ticker.update(turn, (int64_t)c[0]);
+            events->send(Event::turn_complete(turn));
+        } else {
+            const int64_t n = std::min<int64_t>(chunk, p.Turns - turn);
+            const auto t0 = std::chrono::steady_clock::now();
+            const std::vector<uint64_t> c = eng->step(n, true);
+            for (int64_t i = 0; i < n; ++i) {
+                ticker.update(turn + (int)i + 1, (int64_t)c[(size_t)i]);
+                events->send(Event::turn_complete(turn + (int)i + 1));
+            }
+            turn += (int)n;
+            // chunk sized on device time + event delivery, so keys wait at most ~chunk_seconds
+            const double dt =
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            if (dt < o.chunk_seconds && chunk < (1 << 20)) chunk *= 2;
+            if (dt > 4 * o.chunk_seconds && chunk > 1) chunk /= 2;
+        }
+    }
+
+    if (quit) {  // 'q' / 'k': FinalTurnComplete with no cells (gol/distributor.go:128,147)
+        ticker.halt();
+        events->send(Event::final_turn_complete(turn, {}));
+        events->close();
+        return;
+    }
+
+    std::vector<Cell> alive = to_cells(eng->alive_cells());  // gol/distributor.go:235
+    ticker.halt();
+    events->send(Event::final_turn_complete(turn, std::move(alive)));
+    snapshot(*eng, p, o, name + "x" + std::to_string(p.Turns));  // out/WxHxT.pgm (:246-253)
+    events->send(Event::state_change(turn, State::Quitting));   // :259
+    events->close();                                             // :262
+}
+
+int Publish(const Request &req, Response *res, int ngpus) {
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, std::unique_ptr<Engine>> cache;
+    const int n = req.ImageSize;
+    if (n <= 0 || (int)req.World.size() != n) return GOLHIP_ERR_ARG;
+    std::vector<uint8_t> cells((size_t)n * n);
+    for (int y = 0; y < n; ++y) {
+        if ((int)req.World[y].size() != n) return GOLHIP_ERR_ARG;
+        std::copy(req.World[y].begin(), req.World[y].end(), cells.begin() + (long)y * n);
+    }
+    std::lock_guard<std::mutex> lk(mu);
+    auto &eng = cache[{n, ngpus}];
+    if (!eng) eng = std::make_unique<Engine>(n, n, ngpus, 1);
+    eng->load(cells);
+    eng->step(1, false);
+    const std::vector<uint8_t> out = eng->store();
+    res->InitialWorld = req.World;  // broker/broker.go:158
+    res->World.assign(n, std::vector<uint8_t>(n));
+    for (int y = 0; y < n; ++y)
+        std::copy(out.begin() + (long)y * n, out.begin() + (long)(y + 1) * n, res->World[y].begin());
+    res->Turn = 1;
+    return GOLHIP_OK;
+}
+
+}  // namespace gol

@@ -1,0 +1,120 @@
+// gol.hpp -- C++ host mirror of the reference's public contract (package gol):
+//
+//   Params                      gol/gol.go:6-11
+//   Run(p, events, keyPresses)  gol/gol.go:14-57   (distributor: gol/distributor.go:194-263)
+//   Event + event kinds         gol/event.go:9-68  (String / GetCompletedTurns)
+//   util.Cell                   util/cell.go:4-6
+//   stubs Request / Response    stubs/stubs.go:15-29 (kept as value types for callers that
+//                               speak the broker protocol; the engine answers Publish in-process)
+//
+// The reference is Go; there is no Go toolchain on this image, so the host side above the C ABI
+// (include/golhip.h) is C++ (see INTEGRATION.md for the cgo binding a Go maintainer would add).
+// Run() drives libgolhip instead of dialling the broker (gol/distributor.go:218-222): the board
+// stays in HBM and the turn loop calls golhip_step in chunks so that the 2 s AliveCellsCount
+// ticker and the p/s/q/k keys are serviced between chunks.
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "channel.hpp"
+
+namespace gol {
+
+// util/cell.go:4-6
+struct Cell {
+    int X = 0, Y = 0;
+    bool operator==(const Cell &o) const { return X == o.X && Y == o.Y; }
+    bool operator<(const Cell &o) const { return Y != o.Y ? Y < o.Y : X < o.X; }
+};
+
+// gol/gol.go:6-11
+struct Params {
+    int Turns = 0;
+    int Threads = 1;  // kept for contract parity; the GPU grid replaces goroutine strips
+    int ImageWidth = 0;
+    int ImageHeight = 0;
+};
+
+// gol/event.go:32-38
+enum class State { Paused, Executing, Quitting };
+std::string to_string(State s);
+
+// gol/event.go:19-68 -- one tagged struct instead of Go's interface of value types.
+enum class EventKind {
+    AliveCellsCount,      // CompletedTurns, CellsCount
+    ImageOutputComplete,  // CompletedTurns, Filename
+    StateChange,          // CompletedTurns, NewState
+    CellFlipped,          // CompletedTurns, Cell
+    TurnComplete,         // CompletedTurns
+    FinalTurnComplete,    // CompletedTurns, Alive
+};
+
+struct Event {
+    EventKind kind = EventKind::TurnComplete;
+    int CompletedTurns = 0;
+    int64_t CellsCount = 0;
+    std::string Filename;
+    State NewState = State::Executing;
+    Cell cell;
+    std::shared_ptr<std::vector<Cell>> Alive;  // FinalTurnComplete only
+
+    // gol/event.go:71-131: the GUI prints events whose String() is non-empty (sdl/loop.go:44-47)
+    std::string String() const;
+    int GetCompletedTurns() const { return CompletedTurns; }
+
+    static Event alive_cells_count(int turns, int64_t n);
+    static Event image_output_complete(int turns, std::string f);
+    static Event state_change(int turns, State s);
+    static Event cell_flipped(int turns, Cell c);
+    static Event turn_complete(int turns);
+    static Event final_turn_complete(int turns, std::vector<Cell> alive);
+};
+
+// stubs/stubs.go:15-29 (the broker wire types; World rows of 0/255 bytes)
+struct Request {
+    std::vector<std::vector<uint8_t>> World;
+    int ImageSize = 0, SplitSize = 0, StartY = 0, EndY = 0, Threads = 0;
+};
+struct Response {
+    std::vector<std::vector<uint8_t>> World;
+    int Turn = 0;
+    std::vector<Cell> FlipCells;
+    std::vector<std::vector<uint8_t>> InitialWorld;
+};
+
+// Engine-side options (no reference equivalent; defaults reproduce the reference's behaviour).
+struct RunOptions {
+    std::string image_dir = "images";  // gol/io.go:96  images/<W>x<H>.pgm
+    std::string out_dir = "out";       // gol/io.go:43  out/<name>.pgm
+    int ngpus = 1;                     // row strips over this many GPUs
+    int k = 8;                         // temporal-blocking depth when no per-turn flips are needed
+    bool flip_events = true;           // per-turn CellFlipped (gol/distributor.go:53-59)
+    int ticker_ms = 2000;              // AliveCellsCount period (gol/distributor.go:228)
+    double chunk_seconds = 0.02;       // target device time per step chunk (key/ticker latency)
+};
+
+// gol/gol.go:14 -- runs the whole simulation, sends events, closes `events` at the end.
+// keyPresses may be null (the tests pass nil, gol_test.go:34).
+void Run(Params p, Channel<Event> *events, Channel<char> *keyPresses,
+         const RunOptions &opts = RunOptions());
+
+// Broker.Publish equivalent (broker/broker.go:157-180): one turn of req.World on the GPU.
+// res.InitialWorld = req.World, res.World = next generation.
+int Publish(const Request &req, Response *res, int ngpus = 1);
+
+// Forget a board saved by 'q' (broker/broker.go:124-141 CheckStates clears `paused`).
+void reset_saved_state();
+
+// gol/io.go helpers (P5, maxval 255).
+struct Image {
+    int width = 0, height = 0;
+    std::vector<uint8_t> pixels;  // row-major, width*height
+};
+Image read_pgm(const std::string &path);                       // gol/io.go:90-128
+void write_pgm(const std::string &path, const Image &img);     // gol/io.go:42-87
+std::vector<Cell> alive_cells_of(const Image &img);            // gol/distributor.go:153-166
+
+}  // namespace gol

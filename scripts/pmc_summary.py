@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc CSVs of scripts/pmc_passes.sh into per-launch numbers.
+
+HBM bytes follow MI355X_MICROARCH.md (HBM section): FETCH_SIZE/WRITE_SIZE are in KiB; on gfx950
+FETCH_SIZE under-counts wide streaming reads by 2x and other widths are uncalibrated, so the read
+and write scales are CALIBRATED here on two kernels of known traffic that use the stencil's own
+access width (4-byte lanes): popcount_rows reads exactly the board once, init_random_rows writes
+exactly the board once.
+Usage: pmc_summary.py <pmc dir> <k> <board bytes> [<json out> <key>]
+"""
+import csv
+import glob
+import json
+import sys
+from collections import defaultdict
+
+
+def load(d):
+    rows = []
+    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        rows += list(csv.DictReader(open(f)))
+    return rows
+
+
+def main():
+    d, k, board = sys.argv[1], int(sys.argv[2]), float(sys.argv[3])
+    per = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> values per dispatch
+    for r in load(d):
+        name = r.get("Kernel_Name", "")
+        short = ("stencil" if "gol_stencil" in name else "popcount" if "popcount_rows" in name
+                 else "init" if "init_random" in name else None)
+        if short:
+            per[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    avg = {kn: {c: sum(v) / len(v) for c, v in cs.items()} for kn, cs in per.items()}
+    out = {"k": k, "board_bytes": board, "avg_per_dispatch": avg}
+    try:
+        rscale = board / (avg["popcount"]["FETCH_SIZE"] * 1024)
+        wscale = board / (avg["init"]["WRITE_SIZE"] * 1024)
+        fetch = avg["stencil"]["FETCH_SIZE"] * 1024 * rscale
+        write = avg["stencil"]["WRITE_SIZE"] * 1024 * wscale
+        out.update({"read_scale": rscale, "write_scale": wscale,
+                    "stencil_read_bytes": fetch, "stencil_write_bytes": write,
+                    "hbm_bytes_per_launch": fetch + write,
+                    "algorithmic_bytes_per_launch": 0.25 * board * 8 * k})
+    except KeyError as e:
+        out["error"] = f"missing {e}"
+    print(json.dumps(out, indent=1))
+    if len(sys.argv) > 5:
+        try:
+            allj = json.load(open(sys.argv[4]))
+        except Exception:
+            allj = {}
+        allj[sys.argv[5]] = out
+        json.dump(allj, open(sys.argv[4], "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
