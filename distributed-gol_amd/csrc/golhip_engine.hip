@@ -254,30 +254,59 @@ int timing_collect(golhip_t h) {
     return GOLHIP_OK;
 }
 
-// Exchange K halo rows between neighbouring strips (toroidal ring) on the comm streams.
+// The 4 transfers of a K-row exchange for one strip (toroidal ring of strips).  Order matters
+// when up == down (world 2): sends to `down` first and receives from `up` first, so the i-th send
+// of one rank to a peer matches the i-th receive of that peer (RCCL per-peer ordering).
+void halo_plan(int world, int rank, int64_t rows, int K, golhip_xfer out[4]) {
+    const int up = (rank - 1 + world) % world, down = (rank + 1) % world;
+    out[0] = {0, down, rows - K, K};  // my last K rows -> the top halo of the strip below
+    out[1] = {0, up, 0, K};           // my first K rows -> the bottom halo of the strip above
+    out[2] = {1, up, -(int64_t)K, K}; // top halo <- last K rows of the strip above
+    out[3] = {1, down, rows, K};      // bottom halo <- first K rows of the strip below
+}
+
+// Exchange K halo rows between neighbouring strips on the comm streams.
+//  * rank mode (one process per GPU): RCCL send/recv over xGMI, the plan above in one group;
+//  * single process (golhip_create / golhip_create_strips): every strip pulls its two halos from
+//    its neighbours' rows with peer copies (xGMI between devices, a D2D copy on one device).
 int exchange_halos(golhip_t h, int K) {
-    const int W = h->world_size;
     const size_t bytes = (size_t)K * (size_t)h->pitch * sizeof(uint32_t);
     for (auto &s : h->shards) {
         HIPCHK(h, hipSetDevice(s.device));
         HIPCHK(h, hipEventRecord(s.ev_ready, s.compute));
-        HIPCHK(h, hipStreamWaitEvent(s.comm, s.ev_ready, 0));
     }
-    NCCLCHK(h, ncclGroupStart());
-    for (auto &s : h->shards) {
-        const int up = (s.rank - 1 + W) % W, down = (s.rank + 1) % W;
-        uint32_t *r0 = h->row0(s, h->cur);
-        // Order matters when up == down (W == 2): sends to `down` first, receives from `up`
-        // first, so the i-th send of one rank matches the i-th receive of its peer.
-        NCCLCHK(h, ncclSend(r0 + (s.rows - K) * h->pitch, bytes, ncclUint8, down, s.comm_nccl,
-                            s.comm));
-        NCCLCHK(h, ncclSend(r0, bytes, ncclUint8, up, s.comm_nccl, s.comm));
-        NCCLCHK(h, ncclRecv(r0 - (int64_t)K * h->pitch, bytes, ncclUint8, up, s.comm_nccl,
-                            s.comm));
-        NCCLCHK(h, ncclRecv(r0 + s.rows * h->pitch, bytes, ncclUint8, down, s.comm_nccl,
-                            s.comm));
+    if (h->rank_mode) {
+        for (auto &s : h->shards) HIPCHK(h, hipStreamWaitEvent(s.comm, s.ev_ready, 0));
+        NCCLCHK(h, ncclGroupStart());
+        for (auto &s : h->shards) {
+            golhip_xfer plan[4];
+            halo_plan(h->world_size, s.rank, s.rows, K, plan);
+            uint32_t *r0 = h->row0(s, h->cur);
+            for (const golhip_xfer &x : plan) {
+                uint32_t *p = r0 + x.row * h->pitch;
+                if (x.kind == 0)
+                    NCCLCHK(h, ncclSend(p, bytes, ncclUint8, x.peer, s.comm_nccl, s.comm));
+                else
+                    NCCLCHK(h, ncclRecv(p, bytes, ncclUint8, x.peer, s.comm_nccl, s.comm));
+            }
+        }
+        NCCLCHK(h, ncclGroupEnd());
+    } else {
+        const int n = (int)h->shards.size();
+        for (int i = 0; i < n; ++i) {
+            Shard &s = h->shards[i];
+            Shard &up = h->shards[(i - 1 + n) % n], &down = h->shards[(i + 1) % n];
+            HIPCHK(h, hipSetDevice(s.device));
+            HIPCHK(h, hipStreamWaitEvent(s.comm, up.ev_ready, 0));
+            HIPCHK(h, hipStreamWaitEvent(s.comm, down.ev_ready, 0));
+            uint32_t *r0 = h->row0(s, h->cur);
+            HIPCHK(h, hipMemcpyPeerAsync(r0 - (int64_t)K * h->pitch, s.device,
+                                         h->row0(up, h->cur) + (up.rows - K) * h->pitch, up.device,
+                                         bytes, s.comm));
+            HIPCHK(h, hipMemcpyPeerAsync(r0 + s.rows * h->pitch, s.device, h->row0(down, h->cur),
+                                         down.device, bytes, s.comm));
+        }
     }
-    NCCLCHK(h, ncclGroupEnd());
     for (auto &s : h->shards) {
         HIPCHK(h, hipSetDevice(s.device));
         HIPCHK(h, hipEventRecord(s.ev_halo, s.comm));
@@ -343,16 +372,25 @@ int sync_all(golhip_t h) {
     return GOLHIP_OK;
 }
 
-// Sum n uint64 values (device, per shard) over every rank; result in shard 0's buffer.
-int allreduce_u64(golhip_t h, std::vector<unsigned long long *> bufs, size_t n) {
-    if (h->world_size == 1) return GOLHIP_OK;
-    NCCLCHK(h, ncclGroupStart());
-    for (size_t i = 0; i < h->shards.size(); ++i) {
-        Shard &s = h->shards[i];
-        NCCLCHK(h, ncclAllReduce(bufs[i], bufs[i], n, ncclUint64, ncclSum, s.comm_nccl,
+// Sum n uint64 device values over every strip of the board into host memory `out`:
+// strips of this process are summed on the host, ranks with one ncclAllReduce.
+int reduce_u64(golhip_t h, const std::vector<unsigned long long *> &bufs, size_t n, uint64_t *out) {
+    if (h->rank_mode && h->world_size > 1) {
+        Shard &s = h->shards[0];
+        HIPCHK(h, hipSetDevice(s.device));
+        NCCLCHK(h, ncclAllReduce(bufs[0], bufs[0], n, ncclUint64, ncclSum, s.comm_nccl,
                                  s.compute));
     }
-    NCCLCHK(h, ncclGroupEnd());
+    std::vector<uint64_t> tmp(n);
+    for (size_t i = 0; i < h->shards.size(); ++i) {
+        Shard &s = h->shards[i];
+        HIPCHK(h, hipSetDevice(s.device));
+        HIPCHK(h, hipMemcpyAsync(i == 0 ? out : tmp.data(), bufs[i], n * sizeof(uint64_t),
+                                 hipMemcpyDeviceToHost, s.compute));
+        HIPCHK(h, hipStreamSynchronize(s.compute));
+        if (i > 0)
+            for (size_t j = 0; j < n; ++j) out[j] += tmp[j];
+    }
     return GOLHIP_OK;
 }
 
@@ -500,6 +538,15 @@ int golhip_strip_bounds(int64_t height, int world_size, int rank, int64_t *y0, i
     return GOLHIP_OK;
 }
 
+int golhip_halo_plan(int64_t height, int world_size, int rank, int k, golhip_xfer *out) {
+    if (height <= 0 || world_size <= 1 || rank < 0 || rank >= world_size || !out) return GOLHIP_ERR_ARG;
+    if (k < 1 || k > golhip::kMaxK || height / world_size < k) return GOLHIP_ERR_ARG;
+    int64_t y0, rows;
+    strip_bounds(height, world_size, rank, y0, rows);
+    halo_plan(world_size, rank, rows, k, out);
+    return GOLHIP_OK;
+}
+
 int golhip_nccl_unique_id(uint8_t *out) {
     if (!out) return GOLHIP_ERR_ARG;
     ncclUniqueId id;
@@ -509,40 +556,50 @@ int golhip_nccl_unique_id(uint8_t *out) {
     return GOLHIP_OK;
 }
 
-int golhip_create(int width, int height, int ngpus, int k, golhip_t *out) {
+int golhip_create_strips(int width, int height, int nstrips, int ndevices, int k, golhip_t *out) {
     if (!out) return GOLHIP_ERR_ARG;
     *out = nullptr;
-    int rc = validate_geometry(width, height, ngpus, k);
+    int rc = validate_geometry(width, height, nstrips, k);
     if (rc) return rc;
+    if (ndevices < 1 || ndevices > nstrips) return GOLHIP_ERR_ARG;
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < ngpus) return GOLHIP_ERR_NODEV;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < ndevices) return GOLHIP_ERR_NODEV;
     golhip_t h = new golhip_engine();
-    setup_engine(h, width, height, ngpus, k);
-    h->shards.resize(ngpus);
-    for (int r = 0; r < ngpus; ++r) {
+    setup_engine(h, width, height, nstrips, k);
+    h->shards.resize(nstrips);
+    for (int r = 0; r < nstrips; ++r) {
         Shard &s = h->shards[r];
-        s.device = r;
+        s.device = (int)((int64_t)r * ndevices / nstrips);
         s.rank = r;
-        strip_bounds(height, ngpus, r, s.y0, s.rows);
-        if ((rc = check_device_arch(h, r))) goto fail;
+        strip_bounds(height, nstrips, r, s.y0, s.rows);
+    }
+    for (int d = 0; d < ndevices; ++d)
+        if ((rc = check_device_arch(h, d))) goto fail;
+    // peer access between neighbouring devices for the halo copies (xGMI)
+    for (int d = 0; d < ndevices && ndevices > 1; ++d) {
+        for (int e : {(d + 1) % ndevices, (d - 1 + ndevices) % ndevices}) {
+            int can = 0;
+            if (e == d || hipDeviceCanAccessPeer(&can, d, e) != hipSuccess || !can) continue;
+            (void)hipSetDevice(d);
+            hipError_t pe = hipDeviceEnablePeerAccess(e, 0);
+            if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) {
+                rc = fail(h, GOLHIP_ERR_HIP, "peer access %d->%d: %s", d, e, hipGetErrorString(pe));
+                goto fail;
+            }
+            (void)hipGetLastError();
+        }
     }
     if ((rc = create_common(h))) goto fail;
-    if (ngpus > 1) {
-        std::vector<ncclComm_t> comms(ngpus);
-        std::vector<int> devs(ngpus);
-        std::iota(devs.begin(), devs.end(), 0);
-        if (ncclCommInitAll(comms.data(), ngpus, devs.data()) != ncclSuccess) {
-            rc = GOLHIP_ERR_RCCL;
-            goto fail;
-        }
-        for (int r = 0; r < ngpus; ++r) h->shards[r].comm_nccl = comms[r];
-    }
     *out = h;
     return GOLHIP_OK;
 fail:
     for (auto &s : h->shards) free_shard(s);
     delete h;
     return rc;
+}
+
+int golhip_create(int width, int height, int ngpus, int k, golhip_t *out) {
+    return golhip_create_strips(width, height, ngpus, ngpus, k, out);
 }
 
 int golhip_create_rank(int width, int height, int rank, int world_size, int device, int k,
@@ -717,14 +774,8 @@ int golhip_step(golhip_t h, int64_t turns, uint64_t *alive_per_turn) {
     if (counting) {
         std::vector<unsigned long long *> bufs;
         for (auto &s : h->shards) bufs.push_back(s.d_counts);
-        // sum the strips of this handle on shard 0 (single-process multi-GPU) ...
-        int rc = allreduce_u64(h, bufs, (size_t)turns);  // ... and over ranks
+        int rc = reduce_u64(h, bufs, (size_t)turns, alive_per_turn);
         if (rc) return rc;
-        Shard &s0 = h->shards[0];
-        HIPCHK(h, hipSetDevice(s0.device));
-        HIPCHK(h, hipMemcpyAsync(alive_per_turn, s0.d_counts, sizeof(uint64_t) * (size_t)turns,
-                                 hipMemcpyDeviceToHost, s0.compute));
-        HIPCHK(h, hipStreamSynchronize(s0.compute));
         const uint64_t rep = (uint64_t)h->rep();
         if (rep > 1)
             for (int64_t i = 0; i < turns; ++i) alive_per_turn[i] /= rep;
@@ -742,14 +793,10 @@ int golhip_alive_count(golhip_t h, uint64_t *out) {
                                           s.scratch_u64, s.compute));
         bufs.push_back(s.scratch_u64);
     }
-    int rc = allreduce_u64(h, bufs, 1);
+    uint64_t v = 0;
+    int rc = reduce_u64(h, bufs, 1, &v);
     if (rc) return rc;
-    unsigned long long v = 0;
-    Shard &s0 = h->shards[0];
-    HIPCHK(h, hipSetDevice(s0.device));
-    HIPCHK(h, hipMemcpyAsync(&v, s0.scratch_u64, sizeof v, hipMemcpyDeviceToHost, s0.compute));
-    HIPCHK(h, hipStreamSynchronize(s0.compute));
-    *out = v / (unsigned long long)h->rep();
+    *out = v / (uint64_t)h->rep();
     return GOLHIP_OK;
 }
 

@@ -33,7 +33,8 @@ DENSITY_HALF = 0x80000000
 # Every symbol include/golhip.h declares (tests/test_boundary.py checks the .so exports them).
 EXPORTS = [
     "golhip_version", "golhip_strerror", "golhip_device_count", "golhip_strip_bounds",
-    "golhip_create", "golhip_nccl_unique_id", "golhip_create_rank", "golhip_destroy",
+    "golhip_halo_plan",
+    "golhip_create", "golhip_create_strips", "golhip_nccl_unique_id", "golhip_create_rank", "golhip_destroy",
     "golhip_last_error", "golhip_get_info", "golhip_load_bytes", "golhip_init_random",
     "golhip_store_bytes", "golhip_store_words", "golhip_load_words", "golhip_step",
     "golhip_alive_count", "golhip_alive_cells", "golhip_flips", "golhip_turn",
@@ -46,6 +47,11 @@ class GolHipError(RuntimeError):
     def __init__(self, code: int, msg: str):
         super().__init__(f"golhip error {code}: {msg}")
         self.code = code
+
+
+class Xfer(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("peer", ctypes.c_int32), ("row", ctypes.c_int64),
+                ("nrows", ctypes.c_int64)]
 
 
 class Info(ctypes.Structure):
@@ -77,7 +83,9 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
         "golhip_strerror": ([i32], ctypes.c_char_p),
         "golhip_device_count": ([ctypes.POINTER(i32)], i32),
         "golhip_strip_bounds": ([i64, i32, i32, i64p, i64p], i32),
+        "golhip_halo_plan": ([i64, i32, i32, i32, ctypes.POINTER(Xfer)], i32),
         "golhip_create": ([i32, i32, i32, i32, ctypes.POINTER(H)], i32),
+        "golhip_create_strips": ([i32, i32, i32, i32, i32, ctypes.POINTER(H)], i32),
         "golhip_nccl_unique_id": ([ctypes.c_char_p], i32),
         "golhip_create_rank": ([i32, i32, i32, i32, i32, i32, ctypes.c_char_p, ctypes.POINTER(H)], i32),
         "golhip_destroy": ([H], i32),
@@ -123,6 +131,15 @@ def strip_bounds(height: int, world_size: int, rank: int) -> tuple[int, int]:
     return y0.value, rows.value
 
 
+def halo_plan(height: int, world_size: int, rank: int, k: int) -> list[tuple[str, int, int, int]]:
+    """The engine's 4 halo transfers for `rank`, in issue order: (send|recv, peer, row, nrows)."""
+    arr = (Xfer * 4)()
+    rc = load_library().golhip_halo_plan(height, world_size, rank, k, arr)
+    if rc != OK:
+        raise GolHipError(rc, "halo_plan: invalid arguments")
+    return [("send" if x.kind == 0 else "recv", x.peer, x.row, x.nrows) for x in arr]
+
+
 def nccl_unique_id() -> bytes:
     buf = ctypes.create_string_buffer(NCCL_ID_BYTES)
     rc = load_library().golhip_nccl_unique_id(buf)
@@ -135,11 +152,14 @@ class Engine:
     """One libgolhip handle.  Mirrors the broker's role: the board lives on the GPU(s)."""
 
     def __init__(self, width: int, height: int, ngpus: int = 1, k: int = 1, *, rank: int | None = None,
-                 world_size: int = 1, device: int = 0, nccl_id: bytes | None = None):
+                 world_size: int = 1, device: int = 0, nccl_id: bytes | None = None,
+                 strips: int | None = None):
         L = load_library()
         self._L = L
         self._h = ctypes.c_void_p()
-        if rank is None:
+        if strips is not None:
+            rc = L.golhip_create_strips(width, height, strips, ngpus, k, ctypes.byref(self._h))
+        elif rank is None:
             rc = L.golhip_create(width, height, ngpus, k, ctypes.byref(self._h))
         else:
             rc = L.golhip_create_rank(width, height, rank, world_size, device, k, nccl_id,

@@ -71,11 +71,28 @@ int golhip_device_count(int *out);        /* visible HIP devices */
 /* Pure host helper: the row strip of `rank` when `height` rows are split over world_size GPUs. */
 int golhip_strip_bounds(int64_t height, int world_size, int rank, int64_t *y0, int64_t *rows);
 
+/* One transfer of the halo exchange, in the order the engine issues it inside one RCCL group
+ * (kind 0 = send, 1 = receive; rows relative to the strip's row 0, negative = top halo).
+ * With world_size == 2 both neighbours are the same peer: RCCL matches the i-th send of a rank
+ * to a peer with the i-th receive of that peer, which this order keeps consistent. */
+typedef struct {
+    int32_t kind;
+    int32_t peer;
+    int64_t row;
+    int64_t nrows;
+} golhip_xfer;
+/* Pure host helper: the 4 transfers of `rank` for a k-row exchange (out[4]). */
+int golhip_halo_plan(int64_t height, int world_size, int rank, int k, golhip_xfer *out);
+
 /* ---- lifetime --------------------------------------------------------------------------- */
-/* One process, `ngpus` devices (0..ngpus-1), row strips with RCCL halo exchange between them
- * (the on-node replacement of the broker + 4 servers, broker/broker.go:191-205). k = max
- * generations per stencil launch (1..32). */
+/* One process, `ngpus` devices (0..ngpus-1), one row strip each
+ * (the on-node replacement of the broker + 4 servers, broker/broker.go:191-205), halos moved by
+ * peer copies over xGMI. k = max generations per stencil launch (1..32). */
 int golhip_create(int width, int height, int ngpus, int k, golhip_t *out);
+/* One process, `nstrips` row strips placed on devices 0..ndevices-1 (strip s on device
+ * s*ndevices/nstrips), halos by peer copies.  golhip_create(w, h, n, k) == create_strips(w, h, n, n, k);
+ * nstrips > ndevices exercises the multi-strip path on fewer GPUs. */
+int golhip_create_strips(int width, int height, int nstrips, int ndevices, int k, golhip_t *out);
 /* One process per GPU: rank `rank` of `world_size`, on HIP device `device`. nccl_id: the
  * GOLHIP_NCCL_ID_BYTES produced by golhip_nccl_unique_id() on rank 0 (NULL if world_size == 1). */
 int golhip_nccl_unique_id(uint8_t *out /* GOLHIP_NCCL_ID_BYTES */);

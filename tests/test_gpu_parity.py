@@ -119,3 +119,46 @@ def test_cap_error_reports_required_count(golhip, oracle):
         buf = np.empty((10, 2), np.int32)
         rc = e._L.golhip_alive_cells(e._h, buf.ctypes.data, 10, ctypes.byref(n))
         assert rc == golhip.ERR_CAP and n.value == 2819
+
+
+@pytest.mark.parametrize("strips", [2, 3, 4, 8])
+@pytest.mark.parametrize("k", [1, 4, 8, 16])
+def test_row_strips_with_halo_exchange(golhip, oracle, strips, k):
+    """The multi-strip path (halo rows, interior/boundary launches, exchange, count reduction)
+    with several strips on the box's one GPU; must equal the single-board oracle bit for bit."""
+    w, h = 640, 37 * strips + 5
+    if h // strips < k:
+        pytest.skip("strip shorter than k")
+    words = oracle.init_random(w, h, seed=strips * 100 + k)
+    turns = 3 * k + 1
+    with golhip.Engine(w, h, ngpus=1, k=k, strips=strips) as e:
+        assert e.info.world_size == strips and e.info.halo_rows == k
+        e.load_words(words)
+        counts = e.step(turns, counts=True)
+        got = e.store_words()
+        cells = e.alive_cells()
+        n = e.alive_count()
+        e.step(1)
+        flips = e.flips()
+        after = e.store_words()
+    ref = words.copy()
+    ref_counts = oracle.packed_run_words(ref, turns)
+    assert np.array_equal(got, ref)
+    assert np.array_equal(counts.astype(np.int64), ref_counts)
+    board = oracle.unpack(ref, w)
+    assert [tuple(c) for c in cells.tolist()] == oracle.alive_cells(board)
+    assert n == len(cells)
+    ref2 = ref.copy()
+    oracle.packed_run_words(ref2, 1)
+    assert np.array_equal(after, ref2)
+    assert [tuple(c) for c in flips.tolist()] == oracle.flips(board, oracle.unpack(ref2, w))
+
+
+def test_row_strips_bytes_roundtrip(golhip, oracle):
+    _, _, board = oracle.read_pgm(REF / "images/512x512.pgm")
+    with golhip.Engine(512, 512, ngpus=1, k=8, strips=4) as e:
+        e.load(board)
+        assert np.array_equal(e.store(), oracle.to_cells(board))
+        e.step(100)
+        out = e.store()
+    assert oracle.pgm_bytes(out) == (REF / "check/images/512x512x100.pgm").read_bytes()
