@@ -56,6 +56,7 @@ struct golhip_engine {
     int32_t wd = 0;
     int world_size = 1;
     int k = 1, halo = 0, band_rows = 0;
+    int variant = golhip::kVariantSkew;
     bool rank_mode = false;
     std::vector<Shard> shards;
     int cur = 0;
@@ -179,6 +180,8 @@ int setup_engine(golhip_t h, int width, int height, int world, int k) {
     h->k = k;
     h->halo = world > 1 ? k : 0;
     if (const char *e = std::getenv("GOLHIP_BAND_ROWS")) h->band_rows = std::atoi(e);
+    if (const char *e = std::getenv("GOLHIP_VARIANT"))
+        h->variant = std::strcmp(e, "chain") == 0 ? golhip::kVariantChain : golhip::kVariantSkew;
     return GOLHIP_OK;
 }
 
@@ -331,18 +334,18 @@ int step_block(golhip_t h, int K, int64_t counts_off) {
         if (rc) return rc;
         if (h->world_size == 1) {
             StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0);
-            HIPCHK(h, golhip::launch_stencil(K, in, out, p, slots, s.compute));
+            HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, p, slots, s.compute));
         } else if (s.rows >= 3 * K) {
             // interior rows need no halo: overlap them with the exchange
             StencilParams pi = make_params(h, s, K, K, s.rows - K, 0, 0);
-            HIPCHK(h, golhip::launch_stencil(K, in, out, pi, slots, s.compute));
+            HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, pi, slots, s.compute));
             HIPCHK(h, hipStreamWaitEvent(s.compute, s.ev_halo, 0));
             StencilParams pb = make_params(h, s, K, 0, K, s.rows - K, s.rows);
-            HIPCHK(h, golhip::launch_stencil(K, in, out, pb, slots, s.compute));
+            HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, pb, slots, s.compute));
         } else {
             HIPCHK(h, hipStreamWaitEvent(s.compute, s.ev_halo, 0));
             StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0);
-            HIPCHK(h, golhip::launch_stencil(K, in, out, p, slots, s.compute));
+            HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, p, slots, s.compute));
         }
         if (stop) HIPCHK(h, hipEventRecord(stop, s.compute));
         if (counts_off >= 0)

@@ -30,9 +30,13 @@ struct StencilParams {
 constexpr int kMaxK = 32;         // generations per launch limit (halo lane = 32 bits)
 constexpr int kCountSlots = 64;   // per-generation count slots (spread the atomics)
 
+// Stencil variants: levels of a step as one dependent chain, or skewed across steps (K-way ILP).
+constexpr int kVariantSkew = 0;
+constexpr int kVariantChain = 1;
+
 // Launch the K-generation stencil (K in {1,2,4,8,16,32}). count_slots (nullable) receives
 // per-generation alive counts in kCountSlots slots per generation.
-hipError_t launch_stencil(int K, const uint32_t *in_row0, uint32_t *out_row0,
+hipError_t launch_stencil(int K, int variant, const uint32_t *in_row0, uint32_t *out_row0,
                           const StencilParams &p, unsigned long long *count_slots,
                           hipStream_t s);
 bool stencil_k_supported(int K);

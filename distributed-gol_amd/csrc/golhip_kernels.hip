@@ -65,7 +65,12 @@ __device__ __forceinline__ uint32_t life_next(uint32_t as, uint32_t acy, uint32_
     return GOL_BOP3(o, t1, mc & t2, kSelect);
 }
 
-template <int K, bool COUNT>
+// SKEW = false: the K levels of one step form one dependent chain (level j+1 consumes the row
+//               level j produced in the same step).
+// SKEW = true : level j consumes the row level j-1 produced in the PREVIOUS step, so the K level
+//               updates of a step are independent (K-way ILP hides VALU/DPP latency); the
+//               pipeline is K-1 steps deeper.
+template <int K, bool COUNT, bool SKEW>
 __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ in,
                                                    uint32_t *__restrict__ out, StencilParams p,
                                                    unsigned long long *__restrict__ slots) {
@@ -116,14 +121,15 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
     uint32_t *orow = out + ya * p.pitch;
 
     // Per-level two-slot ring of (sum, carry, cell) rows; X/Y swap roles every step.
-    uint32_t xs[K], xcy[K], xc[K], ys[K], ycy[K], yc[K], acc[K];
+    uint32_t xs[K], xcy[K], xc[K], ys[K], ycy[K], yc[K], acc[K], pend[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) {
         xs[j] = xcy[j] = xc[j] = ys[j] = ycy[j] = yc[j] = 0;
-        acc[j] = 0;
+        acc[j] = pend[j] = 0;
     }
     const int64_t nrows = yb - ya;
-    const int64_t nsteps = nrows + 2 * K;
+    const int64_t lag = SKEW ? 3 * K - 1 : 2 * K;  // steps before the first stored row
+    const int64_t nsteps = nrows + lag;
 
     // One step: a new level-0 row enters, every level emits one row; the level-K row is stored.
     // PAR 0: above = X, mid = Y, new -> X.  PAR 1: above = Y, mid = X, new -> Y.
@@ -154,18 +160,66 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
         }                                                                                   \
     } while (0)
 
+    // Skewed step: levels in descending order, level j's input is pend[j] (level j-1's output of
+    // the previous step); level j's output overwrites pend[j+1] after level j+1 has read it.
+    // Level j's output row at step st is ya - K + st - 1 - 2j.
+#define GOL_STEP_SKEW(PAR, VIN, SI)                                                         \
+    do {                                                                                    \
+        const int64_t st = (SI);                                                            \
+        _Pragma("unroll") for (int jj = 0; jj < K; ++jj) {                                  \
+            const int j = K - 1 - jj;                                                       \
+            const uint32_t in = j == 0 ? (VIN) : pend[j];                                   \
+            uint32_t ns, ncy;                                                               \
+            row_sum3(in, ns, ncy);                                                          \
+            uint32_t nx;                                                                    \
+            if (PAR == 0) {                                                                 \
+                nx = life_next(xs[j], xcy[j], ys[j], ycy[j], yc[j], ns, ncy);               \
+                xs[j] = ns; xcy[j] = ncy; xc[j] = in;                                       \
+            } else {                                                                        \
+                nx = life_next(ys[j], ycy[j], xs[j], xcy[j], xc[j], ns, ncy);               \
+                ys[j] = ns; ycy[j] = ncy; yc[j] = in;                                       \
+            }                                                                               \
+            if (COUNT) {                                                                    \
+                const int64_t r = st - K - 1 - 2 * j;                                       \
+                if (r >= 0 && r < nrows) acc[j] += __builtin_popcount(nx);                  \
+            }                                                                               \
+            if (j == K - 1) {                                                               \
+                if (st >= lag && st - lag < nrows) {                                        \
+                    if (owned) orow[col] = nx;                                              \
+                    orow += p.pitch;                                                        \
+                }                                                                           \
+            } else {                                                                        \
+                pend[j + 1] = nx;                                                           \
+            }                                                                               \
+        }                                                                                   \
+    } while (0)
+
     uint32_t b0 = load_next(), b1 = load_next(), b2 = load_next(), b3 = load_next();
-    for (int64_t s = 0; s < nsteps; s += 4) {
-        GOL_STEP(0, b0, s);
-        b0 = load_next();
-        GOL_STEP(1, b1, s + 1);
-        b1 = load_next();
-        GOL_STEP(0, b2, s + 2);
-        b2 = load_next();
-        GOL_STEP(1, b3, s + 3);
-        b3 = load_next();
+    if (SKEW) {
+        for (int64_t s = 0; s < nsteps; s += 4) {
+            GOL_STEP_SKEW(0, b0, s);
+            b0 = load_next();
+            GOL_STEP_SKEW(1, b1, s + 1);
+            b1 = load_next();
+            GOL_STEP_SKEW(0, b2, s + 2);
+            b2 = load_next();
+            GOL_STEP_SKEW(1, b3, s + 3);
+            b3 = load_next();
+        }
+    } else {
+        for (int64_t s = 0; s < nsteps; s += 4) {
+            GOL_STEP(0, b0, s);
+            b0 = load_next();
+            GOL_STEP(1, b1, s + 1);
+            b1 = load_next();
+            GOL_STEP(0, b2, s + 2);
+            b2 = load_next();
+            GOL_STEP(1, b3, s + 3);
+            b3 = load_next();
+        }
     }
 #undef GOL_STEP
+#undef GOL_STEP_SKEW
 
     if (COUNT) {
 #pragma unroll
@@ -426,18 +480,18 @@ inline unsigned grid_for(int64_t n, int threads = 256, int64_t cap = 8192) {
     return (unsigned)g;
 }
 
-template <int K>
+template <int K, bool SKEW>
 hipError_t launch_stencil_k(const uint32_t *in, uint32_t *out, const StencilParams &p,
                             unsigned long long *slots, hipStream_t s) {
     const int64_t waves = p.nbands * (int64_t)p.nchunks;
     const unsigned blocks = (unsigned)((waves + 3) / 4);
     if (blocks == 0) return hipSuccess;
     if (slots)
-        hipLaunchKernelGGL((gol_stencil<K, true>), dim3(blocks), dim3(256), 0, s, in, out, p,
-                           slots);
+        hipLaunchKernelGGL((gol_stencil<K, true, SKEW>), dim3(blocks), dim3(256), 0, s, in, out,
+                           p, slots);
     else
-        hipLaunchKernelGGL((gol_stencil<K, false>), dim3(blocks), dim3(256), 0, s, in, out, p,
-                           slots);
+        hipLaunchKernelGGL((gol_stencil<K, false, SKEW>), dim3(blocks), dim3(256), 0, s, in, out,
+                           p, slots);
     return hipGetLastError();
 }
 
@@ -447,17 +501,23 @@ bool stencil_k_supported(int K) {
     return K == 1 || K == 2 || K == 4 || K == 8 || K == 16 || K == 32;
 }
 
-hipError_t launch_stencil(int K, const uint32_t *in_row0, uint32_t *out_row0,
+hipError_t launch_stencil(int K, int variant, const uint32_t *in_row0, uint32_t *out_row0,
                           const StencilParams &p, unsigned long long *slots, hipStream_t s) {
+#define GOL_CASE(KK)                                                                   \
+    case KK:                                                                           \
+        return variant == kVariantChain                                                \
+                   ? launch_stencil_k<KK, false>(in_row0, out_row0, p, slots, s)       \
+                   : launch_stencil_k<KK, true>(in_row0, out_row0, p, slots, s);
     switch (K) {
-        case 1: return launch_stencil_k<1>(in_row0, out_row0, p, slots, s);
-        case 2: return launch_stencil_k<2>(in_row0, out_row0, p, slots, s);
-        case 4: return launch_stencil_k<4>(in_row0, out_row0, p, slots, s);
-        case 8: return launch_stencil_k<8>(in_row0, out_row0, p, slots, s);
-        case 16: return launch_stencil_k<16>(in_row0, out_row0, p, slots, s);
-        case 32: return launch_stencil_k<32>(in_row0, out_row0, p, slots, s);
+        GOL_CASE(1)
+        GOL_CASE(2)
+        GOL_CASE(4)
+        GOL_CASE(8)
+        GOL_CASE(16)
+        GOL_CASE(32)
         default: return hipErrorInvalidValue;
     }
+#undef GOL_CASE
 }
 
 hipError_t launch_count_finalize(int K, unsigned long long *slots, unsigned long long *counts,
