@@ -199,12 +199,16 @@ int pick_k(int n) {
 int64_t auto_band(golhip_t h, int64_t rows_total, int K) {
     if (h->band_rows > 0) return h->band_rows;
     const int64_t nchunks = (h->wd + 61) / 62;
-    // aim for ~4096 waves in flight (16 per CU), bands at least 4K rows tall so the 2K-row
-    // pipeline fill stays small, at most 1024 rows
-    int64_t target_bands = std::max<int64_t>(1, 4096 / nchunks);
-    int64_t band = (rows_total + target_bands - 1) / target_bands;
-    band = std::max<int64_t>(band, std::min<int64_t>(4 * K, rows_total));
-    band = std::max<int64_t>(band, 4);
+    // Fill the chip exactly once: as many waves as can be resident (CUs x resident waves per CU)
+    // so every SIMD gets the same number of equal bands; a band is at least 2K rows (the
+    // pipeline fill of a K-level band is 2K..3K steps) and at most 1024.
+    int cus = 256;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, h->shards[0].device) == hipSuccess) cus = prop.multiProcessorCount;
+    const int64_t capacity = (int64_t)cus * golhip::stencil_waves_per_cu(K, h->variant);
+    int64_t band = (rows_total * nchunks + capacity - 1) / capacity;
+    band = std::max<int64_t>(band, std::min<int64_t>(2 * K, rows_total));
+    band = std::max<int64_t>(band, 1);
     band = std::min<int64_t>(band, 1024);
     return band;
 }

@@ -40,6 +40,8 @@ hipError_t launch_stencil(int K, int variant, const uint32_t *in_row0, uint32_t 
                           const StencilParams &p, unsigned long long *count_slots,
                           hipStream_t s);
 bool stencil_k_supported(int K);
+// Resident waves per CU of the stencil launch (occupancy query), for sizing the grid.
+int stencil_waves_per_cu(int K, int variant);
 // Sum the slots of K generations into counts[0..K) and zero the slots.
 hipError_t launch_count_finalize(int K, unsigned long long *slots, unsigned long long *counts,
                                  hipStream_t s);

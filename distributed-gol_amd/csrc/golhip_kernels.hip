@@ -194,28 +194,20 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
         }                                                                                   \
     } while (0)
 
-    uint32_t b0 = load_next(), b1 = load_next(), b2 = load_next(), b3 = load_next();
-    if (SKEW) {
-        for (int64_t s = 0; s < nsteps; s += 4) {
-            GOL_STEP_SKEW(0, b0, s);
-            b0 = load_next();
-            GOL_STEP_SKEW(1, b1, s + 1);
-            b1 = load_next();
-            GOL_STEP_SKEW(0, b2, s + 2);
-            b2 = load_next();
-            GOL_STEP_SKEW(1, b3, s + 3);
-            b3 = load_next();
-        }
-    } else {
-        for (int64_t s = 0; s < nsteps; s += 4) {
-            GOL_STEP(0, b0, s);
-            b0 = load_next();
-            GOL_STEP(1, b1, s + 1);
-            b1 = load_next();
-            GOL_STEP(0, b2, s + 2);
-            b2 = load_next();
-            GOL_STEP(1, b3, s + 3);
-            b3 = load_next();
+    // Prefetch ring: loads run P steps ahead of their use (deeper for small K, whose steps are
+    // short and would otherwise expose HBM latency).
+    constexpr int P = K >= 4 ? 4 : (K == 2 ? 8 : 16);
+    uint32_t buf[P];
+#pragma unroll
+    for (int u = 0; u < P; ++u) buf[u] = load_next();
+    for (int64_t s = 0; s < nsteps; s += P) {
+#pragma unroll
+        for (int u = 0; u < P; ++u) {
+            if (SKEW)
+                GOL_STEP_SKEW((u & 1), buf[u], s + u);
+            else
+                GOL_STEP((u & 1), buf[u], s + u);
+            buf[u] = load_next();
         }
     }
 #undef GOL_STEP
@@ -518,6 +510,29 @@ hipError_t launch_stencil(int K, int variant, const uint32_t *in_row0, uint32_t 
         default: return hipErrorInvalidValue;
     }
 #undef GOL_CASE
+}
+
+int stencil_waves_per_cu(int K, int variant) {
+    const void *fn = nullptr;
+#define GOL_FN(KK)                                                                           \
+    case KK:                                                                                 \
+        fn = variant == kVariantChain ? (const void *)gol_stencil<KK, false, false>          \
+                                      : (const void *)gol_stencil<KK, false, true>;          \
+        break;
+    switch (K) {
+        GOL_FN(1)
+        GOL_FN(2)
+        GOL_FN(4)
+        GOL_FN(8)
+        GOL_FN(16)
+        GOL_FN(32)
+        default: return 4;
+    }
+#undef GOL_FN
+    int blocks = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, 256, 0) != hipSuccess || blocks < 1)
+        return 4;
+    return blocks * 4;  // 256-thread blocks = 4 waves
 }
 
 hipError_t launch_count_finalize(int K, unsigned long long *slots, unsigned long long *counts,
