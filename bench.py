@@ -41,8 +41,8 @@ BYTES_PER_CELL_UPDATE = 0.25  # 1 packed bit read + 1 packed bit written per cel
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=256, help="timed generations")
-    ap.add_argument("--warmup", type=int, default=32, help="untimed generations")
+    ap.add_argument("--steps", type=int, default=1000, help="timed generations (configs[2]: 1000 turns)")
+    ap.add_argument("--warmup", type=int, default=8, help="untimed generations")
     ap.add_argument("--size", type=int, default=65536, help="board width")
     ap.add_argument("--height", type=int, default=0,
                     help="total board height (default: size * N, weak scaling)")
@@ -52,7 +52,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-sweep", action="store_true", help="skip the k sweep")
     ap.add_argument("--cpu-size", type=int, default=16384)
-    ap.add_argument("--cpu-turns", type=int, default=24)
+    ap.add_argument("--cpu-turns", type=int, default=96)
+    ap.add_argument("--no-timing", action="store_true",
+                    help="no per-launch HIP events in the timed region (roofline from wall time)")
     ap.add_argument("--pmc-file", default=str(ROOT / "profiles" / "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -131,10 +133,13 @@ def main():
     eng.sync()
 
     # timed region: exactly a.steps generations, per-launch HIP events on the compute stream
-    eng.timing(True)
+    eng.timing(not a.no_timing)
     dt = timed_steps(eng, a.steps, world)
     kern_ms, launches, gens = eng.kernel_time()
     eng.timing(False)
+    if a.no_timing:
+        launches = -(-a.steps // a.k)
+        kern_ms, gens = dt * 1e3, a.steps
 
     total_updates = width * height * a.steps
     gcups = total_updates / dt / 1e9

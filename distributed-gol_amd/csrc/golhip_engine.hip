@@ -57,6 +57,8 @@ struct golhip_engine {
     int world_size = 1;
     int k = 1, halo = 0, band_rows = 0;
     int variant = golhip::kVariantSkew;
+    int cus = 0;                 // compute units of the first device (grid sizing)
+    int waves_per_cu[golhip::kMaxK + 1][2] = {};  // occupancy cache per (K, variant)
     bool rank_mode = false;
     std::vector<Shard> shards;
     int cur = 0;
@@ -202,10 +204,15 @@ int64_t auto_band(golhip_t h, int64_t rows_total, int K) {
     // Fill the chip exactly once: as many waves as can be resident (CUs x resident waves per CU)
     // so every SIMD gets the same number of equal bands; a band is at least 2K rows (the
     // pipeline fill of a K-level band is 2K..3K steps) and at most 1024.
-    int cus = 256;
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, h->shards[0].device) == hipSuccess) cus = prop.multiProcessorCount;
-    const int64_t capacity = (int64_t)cus * golhip::stencil_waves_per_cu(K, h->variant);
+    if (h->cus == 0) {
+        hipDeviceProp_t prop;
+        h->cus = hipGetDeviceProperties(&prop, h->shards[0].device) == hipSuccess
+                     ? prop.multiProcessorCount
+                     : 256;
+    }
+    int &wpc = h->waves_per_cu[K][h->variant];
+    if (wpc == 0) wpc = golhip::stencil_waves_per_cu(K, h->variant);
+    const int64_t capacity = (int64_t)h->cus * wpc;
     int64_t band = (rows_total * nchunks + capacity - 1) / capacity;
     band = std::max<int64_t>(band, std::min<int64_t>(2 * K, rows_total));
     band = std::max<int64_t>(band, 1);
