@@ -58,7 +58,7 @@ struct golhip_engine {
     int k = 1, halo = 0, band_rows = 0;
     int variant = golhip::kVariantSkew;
     int cus = 0;                 // compute units of the first device (grid sizing)
-    int waves_per_cu[golhip::kMaxK + 1][2] = {};  // occupancy cache per (K, variant)
+    int waves_per_cu[golhip::kMaxK + 1][golhip::kNumVariants] = {};  // occupancy cache per (K, variant)
     bool rank_mode = false;
     std::vector<Shard> shards;
     int cur = 0;
@@ -183,7 +183,9 @@ int setup_engine(golhip_t h, int width, int height, int world, int k) {
     h->halo = world > 1 ? k : 0;
     if (const char *e = std::getenv("GOLHIP_BAND_ROWS")) h->band_rows = std::atoi(e);
     if (const char *e = std::getenv("GOLHIP_VARIANT"))
-        h->variant = std::strcmp(e, "chain") == 0 ? golhip::kVariantChain : golhip::kVariantSkew;
+        h->variant = std::strcmp(e, "chain") == 0  ? golhip::kVariantChain
+                     : std::strcmp(e, "lds") == 0 ? golhip::kVariantSkewLds
+                                                  : golhip::kVariantSkew;
     return GOLHIP_OK;
 }
 
@@ -340,9 +342,6 @@ int step_block(golhip_t h, int K, int64_t counts_off) {
         unsigned long long *slots = counts_off >= 0 ? s.slots : nullptr;
         const uint32_t *in = h->row0(s, h->cur);
         uint32_t *out = h->row0(s, nxt);
-        hipEvent_t stop = nullptr;
-        int rc = timing_begin(h, s, &stop);
-        if (rc) return rc;
         if (h->world_size == 1) {
             StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0);
             HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, p, slots, s.compute));
@@ -358,7 +357,6 @@ int step_block(golhip_t h, int K, int64_t counts_off) {
             StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0);
             HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, p, slots, s.compute));
         }
-        if (stop) HIPCHK(h, hipEventRecord(stop, s.compute));
         if (counts_off >= 0)
             HIPCHK(h, golhip::launch_count_finalize(K, s.slots, s.d_counts + counts_off,
                                                      s.compute));
@@ -366,10 +364,6 @@ int step_block(golhip_t h, int K, int64_t counts_off) {
     if (h->timing) {
         h->tlaunches += 1;
         h->tgens += K;
-        if (h->tused >= 1024) {
-            int rc = timing_collect(h);
-            if (rc) return rc;
-        }
     }
     h->cur = nxt;
     h->turn += K;
@@ -777,6 +771,14 @@ int golhip_step(golhip_t h, int64_t turns, uint64_t *alive_per_turn) {
             }
         }
     }
+    // Timing: ONE event pair around the whole call on the first strip's compute stream (per-
+    // launch events would add ~10 us of idle GPU between launches); the average launch time is
+    // that span / launches (the launches run back to back on the stream).
+    hipEvent_t stop = nullptr;
+    if (h->timing) {
+        int rc = timing_begin(h, h->shards[0], &stop);
+        if (rc) return rc;
+    }
     int64_t done = 0;
     while (done < turns) {
         const int64_t left = turns - done;
@@ -784,6 +786,14 @@ int golhip_step(golhip_t h, int64_t turns, uint64_t *alive_per_turn) {
         int rc = step_block(h, K, counting ? done : -1);
         if (rc) return rc;
         done += K;
+    }
+    if (stop) {
+        HIPCHK(h, hipSetDevice(h->shards[0].device));
+        HIPCHK(h, hipEventRecord(stop, h->shards[0].compute));
+        if (h->tused >= 1024) {
+            int rc = timing_collect(h);
+            if (rc) return rc;
+        }
     }
     if (counting) {
         std::vector<unsigned long long *> bufs;

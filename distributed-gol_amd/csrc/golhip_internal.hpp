@@ -33,6 +33,8 @@ constexpr int kCountSlots = 64;   // per-generation count slots (spread the atom
 // Stencil variants: levels of a step as one dependent chain, or skewed across steps (K-way ILP).
 constexpr int kVariantSkew = 0;
 constexpr int kVariantChain = 1;
+constexpr int kVariantSkewLds = 2;  // skewed, cross-lane neighbours through ds_bpermute
+constexpr int kNumVariants = 3;
 
 // Launch the K-generation stencil (K in {1,2,4,8,16,32}). count_slots (nullable) receives
 // per-generation alive counts in kCountSlots slots per generation.

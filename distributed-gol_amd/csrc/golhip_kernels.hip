@@ -41,8 +41,18 @@ constexpr uint8_t kTwosIs2 = GOL_TT((c & ~(a | b)) | (~c & a & b));   // p, k, q
 constexpr uint8_t kSelect = GOL_TT((a & b) | (~a & c));               // a ? b : c
 
 // Horizontal 3-cell sum of a row word c (west + self + east) as sum bit s and carry cy.
-__device__ __forceinline__ void row_sum3(uint32_t c, uint32_t &s, uint32_t &cy) {
-    const uint32_t wl = lane_from_west(c), el = lane_from_east(c);
+// XL = 0: neighbour words by DPP (VALU, half rate on gfx950); XL = 1: by ds_bpermute (LDS pipe,
+// frees the VALU; wa/ea = byte addresses of lane-1 / lane+1).
+template <int XL>
+__device__ __forceinline__ void row_sum3(uint32_t c, uint32_t &s, uint32_t &cy, int wa, int ea) {
+    uint32_t wl, el;
+    if (XL == 0) {
+        wl = lane_from_west(c);
+        el = lane_from_east(c);
+    } else {
+        wl = (uint32_t)__builtin_amdgcn_ds_bpermute(wa, (int)c);
+        el = (uint32_t)__builtin_amdgcn_ds_bpermute(ea, (int)c);
+    }
     const uint32_t w = __builtin_amdgcn_alignbit(c, wl, 31);  // cell x-1 moved onto x
     const uint32_t e = __builtin_amdgcn_alignbit(el, c, 1);   // cell x+1 moved onto x
     s = GOL_BOP3(w, c, e, kXor3);
@@ -70,7 +80,7 @@ __device__ __forceinline__ uint32_t life_next(uint32_t as, uint32_t acy, uint32_
 // SKEW = true : level j consumes the row level j-1 produced in the PREVIOUS step, so the K level
 //               updates of a step are independent (K-way ILP hides VALU/DPP latency); the
 //               pipeline is K-1 steps deeper.
-template <int K, bool COUNT, bool SKEW>
+template <int K, bool COUNT, bool SKEW, int XL>
 __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ in,
                                                    uint32_t *__restrict__ out, StencilParams p,
                                                    unsigned long long *__restrict__ slots) {
@@ -92,6 +102,7 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
     const int colraw = (int)chunk * 62 + lane - 1;
     const int col = (colraw + p.wd) % p.wd;
     const bool owned = lane >= 1 && lane <= 62 && colraw < p.wd;
+    const int wa = ((lane - 1) & 63) * 4, ea = ((lane + 1) & 63) * 4;  // ds_bpermute sources
 
     // Input row stream: rows ya-K, ya-K+1, ... (wrap mod H, or clamped to the halo'd strip).
     // Row pointers are wave-uniform (SGPRs); the lane adds its column.
@@ -139,7 +150,7 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
         const int64_t st = (SI);                                                            \
         _Pragma("unroll") for (int j = 0; j < K; ++j) {                                     \
             uint32_t ns, ncy;                                                               \
-            row_sum3(nc, ns, ncy);                                                          \
+            row_sum3<XL>(nc, ns, ncy, wa, ea);                                                          \
             uint32_t nx;                                                                    \
             if (PAR == 0) {                                                                 \
                 nx = life_next(xs[j], xcy[j], ys[j], ycy[j], yc[j], ns, ncy);               \
@@ -170,7 +181,7 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
             const int j = K - 1 - jj;                                                       \
             const uint32_t in = j == 0 ? (VIN) : pend[j];                                   \
             uint32_t ns, ncy;                                                               \
-            row_sum3(in, ns, ncy);                                                          \
+            row_sum3<XL>(in, ns, ncy, wa, ea);                                                        \
             uint32_t nx;                                                                    \
             if (PAR == 0) {                                                                 \
                 nx = life_next(xs[j], xcy[j], ys[j], ycy[j], yc[j], ns, ncy);               \
@@ -472,18 +483,18 @@ inline unsigned grid_for(int64_t n, int threads = 256, int64_t cap = 8192) {
     return (unsigned)g;
 }
 
-template <int K, bool SKEW>
+template <int K, bool SKEW, int XL>
 hipError_t launch_stencil_k(const uint32_t *in, uint32_t *out, const StencilParams &p,
                             unsigned long long *slots, hipStream_t s) {
     const int64_t waves = p.nbands * (int64_t)p.nchunks;
     const unsigned blocks = (unsigned)((waves + 3) / 4);
     if (blocks == 0) return hipSuccess;
     if (slots)
-        hipLaunchKernelGGL((gol_stencil<K, true, SKEW>), dim3(blocks), dim3(256), 0, s, in, out,
-                           p, slots);
+        hipLaunchKernelGGL((gol_stencil<K, true, SKEW, XL>), dim3(blocks), dim3(256), 0, s, in,
+                           out, p, slots);
     else
-        hipLaunchKernelGGL((gol_stencil<K, false, SKEW>), dim3(blocks), dim3(256), 0, s, in, out,
-                           p, slots);
+        hipLaunchKernelGGL((gol_stencil<K, false, SKEW, XL>), dim3(blocks), dim3(256), 0, s, in,
+                           out, p, slots);
     return hipGetLastError();
 }
 
@@ -498,8 +509,10 @@ hipError_t launch_stencil(int K, int variant, const uint32_t *in_row0, uint32_t 
 #define GOL_CASE(KK)                                                                   \
     case KK:                                                                           \
         return variant == kVariantChain                                                \
-                   ? launch_stencil_k<KK, false>(in_row0, out_row0, p, slots, s)       \
-                   : launch_stencil_k<KK, true>(in_row0, out_row0, p, slots, s);
+                   ? launch_stencil_k<KK, false, 0>(in_row0, out_row0, p, slots, s)    \
+                   : variant == kVariantSkewLds                                        \
+                         ? launch_stencil_k<KK, true, 1>(in_row0, out_row0, p, slots, s) \
+                         : launch_stencil_k<KK, true, 0>(in_row0, out_row0, p, slots, s);
     switch (K) {
         GOL_CASE(1)
         GOL_CASE(2)
@@ -516,8 +529,9 @@ int stencil_waves_per_cu(int K, int variant) {
     const void *fn = nullptr;
 #define GOL_FN(KK)                                                                           \
     case KK:                                                                                 \
-        fn = variant == kVariantChain ? (const void *)gol_stencil<KK, false, false>          \
-                                      : (const void *)gol_stencil<KK, false, true>;          \
+        fn = variant == kVariantChain      ? (const void *)gol_stencil<KK, false, false, 0>  \
+             : variant == kVariantSkewLds ? (const void *)gol_stencil<KK, false, true, 1>   \
+                                          : (const void *)gol_stencil<KK, false, true, 0>;  \
         break;
     switch (K) {
         GOL_FN(1)

@@ -139,7 +139,9 @@ int golhip_set_turn(golhip_t h, int64_t turn);
 int golhip_set_k(golhip_t h, int k);                 /* 1..32, <= halo_rows when world_size > 1 */
 int golhip_set_band_rows(golhip_t h, int band_rows); /* 0 = automatic */
 int golhip_sync(golhip_t h);                         /* wait for all queued device work */
-/* Per-launch HIP-event timing of the stencil kernel on the handle's first strip. */
+/* HIP-event timing of golhip_step calls on the handle's first strip (one event pair per call
+ * around its back-to-back stencil launches); kernel_time reports the summed span, the number of
+ * stencil launch blocks and generations. */
 int golhip_timing(golhip_t h, int enable);
 int golhip_kernel_time(golhip_t h, double *total_ms, int64_t *launches, int64_t *generations);
 

@@ -16,7 +16,7 @@ import golhip  # noqa: E402
 size = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 ks = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1,2,4,8,16").split(",")]
 bands = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "0,128,256,363,512").split(",")]
-variants = (sys.argv[4] if len(sys.argv) > 4 else "skew,chain").split(",")
+variants = (sys.argv[4] if len(sys.argv) > 4 else "skew,chain,lds").split(",")
 engines = {}
 for v in variants:
     os.environ["GOLHIP_VARIANT"] = v
