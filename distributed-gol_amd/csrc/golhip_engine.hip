@@ -183,9 +183,10 @@ int setup_engine(golhip_t h, int width, int height, int world, int k) {
     h->halo = world > 1 ? k : 0;
     if (const char *e = std::getenv("GOLHIP_BAND_ROWS")) h->band_rows = std::atoi(e);
     if (const char *e = std::getenv("GOLHIP_VARIANT"))
-        h->variant = std::strcmp(e, "chain") == 0  ? golhip::kVariantChain
-                     : std::strcmp(e, "lds") == 0 ? golhip::kVariantSkewLds
-                                                  : golhip::kVariantSkew;
+        h->variant = std::strcmp(e, "chain") == 0     ? golhip::kVariantChain
+                     : std::strcmp(e, "skew2") == 0  ? golhip::kVariantSkewD2
+                     : std::strcmp(e, "chain2") == 0 ? golhip::kVariantChainD2
+                                                     : golhip::kVariantSkew;
     return GOLHIP_OK;
 }
 
@@ -202,7 +203,8 @@ int pick_k(int n) {
 
 int64_t auto_band(golhip_t h, int64_t rows_total, int K) {
     if (h->band_rows > 0) return h->band_rows;
-    const int64_t nchunks = (h->wd + 61) / 62;
+    const int64_t per = 62 * golhip::variant_words(h->variant);
+    const int64_t nchunks = (h->wd + per - 1) / per;
     // Fill the chip exactly once: as many waves as can be resident (CUs x resident waves per CU)
     // so every SIMD gets the same number of equal bands; a band is at least 2K rows (the
     // pipeline fill of a K-level band is 2K..3K steps) and at most 1024.
@@ -238,7 +240,8 @@ StencilParams make_params(golhip_t h, const Shard &s, int K, int64_t r0b, int64_
     p.lo = -(int64_t)h->halo;
     p.hi = s.rows + h->halo;
     p.wd = h->wd;
-    p.nchunks = (h->wd + 61) / 62;
+    const int per = 62 * golhip::variant_words(h->variant);
+    p.nchunks = (h->wd + per - 1) / per;
     return p;
 }
 

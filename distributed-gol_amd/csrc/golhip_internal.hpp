@@ -24,17 +24,20 @@ struct StencilParams {
     int64_t wrap_rows;   // > 0: single strip holding the whole torus height (row index mod H)
     int64_t lo, hi;      // halo mode: readable input rows [lo, hi) relative to row 0
     int32_t wd;          // words per row of the torus
-    int32_t nchunks;     // 62-word column chunks per row (lanes 1..62 own, 0 and 63 are halo)
+    int32_t nchunks;     // column chunks per row: lanes 1..62 own D words each, 0 and 63 are halo
 };
 
 constexpr int kMaxK = 32;         // generations per launch limit (halo lane = 32 bits)
 constexpr int kCountSlots = 64;   // per-generation count slots (spread the atomics)
 
-// Stencil variants: levels of a step as one dependent chain, or skewed across steps (K-way ILP).
+// Stencil variants: levels of a step as one dependent chain or skewed across steps (K-way ILP),
+// with 1 or 2 words (32 / 64 cells) per lane.
 constexpr int kVariantSkew = 0;
 constexpr int kVariantChain = 1;
-constexpr int kVariantSkewLds = 2;  // skewed, cross-lane neighbours through ds_bpermute
-constexpr int kNumVariants = 3;
+constexpr int kVariantSkewD2 = 2;
+constexpr int kVariantChainD2 = 3;
+constexpr int kNumVariants = 4;
+inline int variant_words(int v) { return v >= kVariantSkewD2 ? 2 : 1; }
 
 // Launch the K-generation stencil (K in {1,2,4,8,16,32}). count_slots (nullable) receives
 // per-generation alive counts in kCountSlots slots per generation.

@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "golhip_internal.hpp"
 
 namespace golhip {
@@ -40,28 +42,33 @@ constexpr uint8_t kTwosIs1 = GOL_TT((a ^ b) & ~c);                    // p, k, q
 constexpr uint8_t kTwosIs2 = GOL_TT((c & ~(a | b)) | (~c & a & b));   // p, k, q -> T == 2
 constexpr uint8_t kSelect = GOL_TT((a & b) | (~a & c));               // a ? b : c
 
-// Horizontal 3-cell sum of a row word c (west + self + east) as sum bit s and carry cy.
-// XL = 0: neighbour words by DPP (VALU, half rate on gfx950); XL = 1: by ds_bpermute (LDS pipe,
-// frees the VALU; wa/ea = byte addresses of lane-1 / lane+1).
-template <int XL>
-__device__ __forceinline__ void row_sum3(uint32_t c, uint32_t &s, uint32_t &cy, int wa, int ea) {
-    uint32_t wl, el;
-    if (XL == 0) {
-        wl = lane_from_west(c);
-        el = lane_from_east(c);
-    } else {
-        wl = (uint32_t)__builtin_amdgcn_ds_bpermute(wa, (int)c);
-        el = (uint32_t)__builtin_amdgcn_ds_bpermute(ea, (int)c);
+// D consecutive 32-bit words of one row held by one lane (D = 1 or 2).
+template <int D>
+struct Words {
+    uint32_t w[D];
+};
+
+// Horizontal 3-cell sums (west + self + east) of a lane's D words as sum bits s and carries cy.
+// The lane's outer neighbour words come from lanes -1 / +1 by DPP (one per side per row, so
+// D = 2 halves the cross-lane ops per word); the 1-bit shifts are v_alignbit funnel shifts.
+template <int D>
+__device__ __forceinline__ void row_sum3(const Words<D> &c, Words<D> &s, Words<D> &cy) {
+    const uint32_t wl = lane_from_west(c.w[D - 1]);
+    const uint32_t el = lane_from_east(c.w[0]);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const uint32_t left = d == 0 ? wl : c.w[d - 1];
+        const uint32_t right = d == D - 1 ? el : c.w[d + 1];
+        const uint32_t w = __builtin_amdgcn_alignbit(c.w[d], left, 31);  // cell x-1 onto x
+        const uint32_t e = __builtin_amdgcn_alignbit(right, c.w[d], 1);  // cell x+1 onto x
+        s.w[d] = GOL_BOP3(w, c.w[d], e, kXor3);
+        cy.w[d] = GOL_BOP3(w, c.w[d], e, kMaj);
     }
-    const uint32_t w = __builtin_amdgcn_alignbit(c, wl, 31);  // cell x-1 moved onto x
-    const uint32_t e = __builtin_amdgcn_alignbit(el, c, 1);   // cell x+1 moved onto x
-    s = GOL_BOP3(w, c, e, kXor3);
-    cy = GOL_BOP3(w, c, e, kMaj);
 }
 
 // B3/S23 from three rows' 3-cell sums: S9 = 9-cell sum including the centre cell mc;
 // alive next iff S9 == 3, or S9 == 4 and the cell is alive (server/server.go:35-52).
-// 8 VALU ops (7 v_bitop3 + 1 v_and).
+// 8 VALU ops per word (7 v_bitop3 + 1 v_and).
 __device__ __forceinline__ uint32_t life_next(uint32_t as, uint32_t acy, uint32_t ms,
                                               uint32_t mcy, uint32_t mc, uint32_t bs,
                                               uint32_t bcy) {
@@ -75,12 +82,63 @@ __device__ __forceinline__ uint32_t life_next(uint32_t as, uint32_t acy, uint32_
     return GOL_BOP3(o, t1, mc & t2, kSelect);
 }
 
+// A row's per-level state: 3-cell sum, carry and the cells themselves.
+template <int D>
+struct RowState {
+    Words<D> s, cy, c;
+};
+
+// One level update: `in` is the new row (below), `above`/`mid` the two previous rows of the level.
+// Writes the next generation of `mid` to nx and stores `in`'s state into `above` (now free).
+template <int D>
+__device__ __forceinline__ void level_update(RowState<D> &above, const RowState<D> &mid,
+                                             const Words<D> &in, Words<D> &nx) {
+    Words<D> ns, ncy;
+    row_sum3<D>(in, ns, ncy);
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+        nx.w[d] = life_next(above.s.w[d], above.cy.w[d], mid.s.w[d], mid.cy.w[d], mid.c.w[d],
+                            ns.w[d], ncy.w[d]);
+    above.s = ns;
+    above.cy = ncy;
+    above.c = in;
+}
+
+template <int D>
+__device__ __forceinline__ uint32_t popc_words(const Words<D> &x) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int d = 0; d < D; ++d) c += __builtin_popcount(x.w[d]);
+    return c;
+}
+
+template <int D>
+__device__ __forceinline__ Words<D> load_words(const uint32_t *p) {
+    Words<D> v;
+    if constexpr (D == 2) {
+        const uint2 t = *reinterpret_cast<const uint2 *>(p);
+        v.w[0] = t.x;
+        v.w[1] = t.y;
+    } else {
+        v.w[0] = *p;
+    }
+    return v;
+}
+
+template <int D>
+__device__ __forceinline__ void store_words(uint32_t *p, const Words<D> &v) {
+    if constexpr (D == 2)
+        *reinterpret_cast<uint2 *>(p) = make_uint2(v.w[0], v.w[1]);
+    else
+        *p = v.w[0];
+}
+
+// The hot kernel.  K = generations per launch, D = words per lane.
 // SKEW = false: the K levels of one step form one dependent chain (level j+1 consumes the row
 //               level j produced in the same step).
 // SKEW = true : level j consumes the row level j-1 produced in the PREVIOUS step, so the K level
-//               updates of a step are independent (K-way ILP hides VALU/DPP latency); the
-//               pipeline is K-1 steps deeper.
-template <int K, bool COUNT, bool SKEW, int XL>
+//               updates of a step are independent (K-way ILP); the pipeline is K-1 steps deeper.
+template <int K, bool COUNT, bool SKEW, int D>
 __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ in,
                                                    uint32_t *__restrict__ out, StencilParams p,
                                                    unsigned long long *__restrict__ slots) {
@@ -99,10 +157,10 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
         ya = p.r1b + (bandi - p.nbands0) * p.band;
         yb = min(ya + p.band, p.r1e);
     }
-    const int colraw = (int)chunk * 62 + lane - 1;
+    // lanes 1..62 own D words each; lanes 0 and 63 are the horizontal halo
+    const int colraw = ((int)chunk * 62 + lane - 1) * D;
     const int col = (colraw + p.wd) % p.wd;
     const bool owned = lane >= 1 && lane <= 62 && colraw < p.wd;
-    const int wa = ((lane - 1) & 63) * 4, ea = ((lane + 1) & 63) * 4;  // ds_bpermute sources
 
     // Input row stream: rows ya-K, ya-K+1, ... (wrap mod H, or clamped to the halo'd strip).
     // Row pointers are wave-uniform (SGPRs); the lane adds its column.
@@ -114,8 +172,8 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
         ly = ly < p.lo ? p.lo : (ly >= p.hi ? p.hi - 1 : ly);
     }
     const uint32_t *lrow = in + ly * p.pitch;
-    auto load_next = [&]() -> uint32_t {
-        const uint32_t v = lrow[col];
+    auto load_next = [&]() -> Words<D> {
+        const Words<D> v = load_words<D>(lrow + col);
         if (p.wrap_rows > 0) {
             if (++ly == p.wrap_rows) {
                 ly = 0;
@@ -131,98 +189,76 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
     };
     uint32_t *orow = out + ya * p.pitch;
 
-    // Per-level two-slot ring of (sum, carry, cell) rows; X/Y swap roles every step.
-    uint32_t xs[K], xcy[K], xc[K], ys[K], ycy[K], yc[K], acc[K], pend[K];
+    // Per level: a two-slot ring (X/Y swap roles every step) and, skewed, the pending input row.
+    RowState<D> X[K], Y[K];
+    Words<D> pend[K];
+    uint32_t acc[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-        xs[j] = xcy[j] = xc[j] = ys[j] = ycy[j] = yc[j] = 0;
-        acc[j] = pend[j] = 0;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            X[j].s.w[d] = X[j].cy.w[d] = X[j].c.w[d] = 0;
+            Y[j].s.w[d] = Y[j].cy.w[d] = Y[j].c.w[d] = 0;
+            pend[j].w[d] = 0;
+        }
+        acc[j] = 0;
     }
     const int64_t nrows = yb - ya;
     const int64_t lag = SKEW ? 3 * K - 1 : 2 * K;  // steps before the first stored row
     const int64_t nsteps = nrows + lag;
 
-    // One step: a new level-0 row enters, every level emits one row; the level-K row is stored.
+    // One step: a new level-0 row enters, every level emits one row, the level-K row is stored.
     // PAR 0: above = X, mid = Y, new -> X.  PAR 1: above = Y, mid = X, new -> Y.
-#define GOL_STEP(PAR, VIN, SI)                                                              \
-    do {                                                                                    \
-        uint32_t nc = (VIN);                                                                \
-        const int64_t st = (SI);                                                            \
-        _Pragma("unroll") for (int j = 0; j < K; ++j) {                                     \
-            uint32_t ns, ncy;                                                               \
-            row_sum3<XL>(nc, ns, ncy, wa, ea);                                                          \
-            uint32_t nx;                                                                    \
-            if (PAR == 0) {                                                                 \
-                nx = life_next(xs[j], xcy[j], ys[j], ycy[j], yc[j], ns, ncy);               \
-                xs[j] = ns; xcy[j] = ncy; xc[j] = nc;                                       \
-            } else {                                                                        \
-                nx = life_next(ys[j], ycy[j], xs[j], xcy[j], xc[j], ns, ncy);               \
-                ys[j] = ns; ycy[j] = ncy; yc[j] = nc;                                       \
-            }                                                                               \
-            if (COUNT) {                                                                    \
-                const int64_t r = st - K - (j + 1); /* level j+1 row - ya */                \
-                if (r >= 0 && r < nrows) acc[j] += __builtin_popcount(nx);                  \
-            }                                                                               \
-            nc = nx;                                                                        \
-        }                                                                                   \
-        if (st >= 2 * K && st - 2 * K < nrows) {                                            \
-            if (owned) orow[col] = nc;                                                      \
-            orow += p.pitch;                                                                \
-        }                                                                                   \
-    } while (0)
-
-    // Skewed step: levels in descending order, level j's input is pend[j] (level j-1's output of
-    // the previous step); level j's output overwrites pend[j+1] after level j+1 has read it.
-    // Level j's output row at step st is ya - K + st - 1 - 2j.
-#define GOL_STEP_SKEW(PAR, VIN, SI)                                                         \
-    do {                                                                                    \
-        const int64_t st = (SI);                                                            \
-        _Pragma("unroll") for (int jj = 0; jj < K; ++jj) {                                  \
-            const int j = K - 1 - jj;                                                       \
-            const uint32_t in = j == 0 ? (VIN) : pend[j];                                   \
-            uint32_t ns, ncy;                                                               \
-            row_sum3<XL>(in, ns, ncy, wa, ea);                                                        \
-            uint32_t nx;                                                                    \
-            if (PAR == 0) {                                                                 \
-                nx = life_next(xs[j], xcy[j], ys[j], ycy[j], yc[j], ns, ncy);               \
-                xs[j] = ns; xcy[j] = ncy; xc[j] = in;                                       \
-            } else {                                                                        \
-                nx = life_next(ys[j], ycy[j], xs[j], xcy[j], xc[j], ns, ncy);               \
-                ys[j] = ns; ycy[j] = ncy; yc[j] = in;                                       \
-            }                                                                               \
-            if (COUNT) {                                                                    \
-                const int64_t r = st - K - 1 - 2 * j;                                       \
-                if (r >= 0 && r < nrows) acc[j] += __builtin_popcount(nx);                  \
-            }                                                                               \
-            if (j == K - 1) {                                                               \
-                if (st >= lag && st - lag < nrows) {                                        \
-                    if (owned) orow[col] = nx;                                              \
-                    orow += p.pitch;                                                        \
-                }                                                                           \
-            } else {                                                                        \
-                pend[j + 1] = nx;                                                           \
-            }                                                                               \
-        }                                                                                   \
-    } while (0)
+    // Chained: level j+1 takes level j's output of this step; level j's output row is
+    //   ya - K + st - (j+1).
+    // Skewed: levels in descending order, level j takes pend[j] (level j-1's output of the
+    //   previous step) and its output overwrites pend[j+1] after level j+1 has read it; level j's
+    //   output row is ya - K + st - 1 - 2j.
+    auto step = [&](auto par, const Words<D> &vin, int64_t st) {
+        constexpr int PAR = decltype(par)::value;
+        Words<D> nc = vin;
+#pragma unroll
+        for (int jj = 0; jj < K; ++jj) {
+            const int j = SKEW ? K - 1 - jj : jj;
+            const Words<D> lin = SKEW ? (j == 0 ? vin : pend[j]) : nc;
+            Words<D> nx;
+            if (PAR == 0)
+                level_update<D>(X[j], Y[j], lin, nx);
+            else
+                level_update<D>(Y[j], X[j], lin, nx);
+            if (COUNT) {
+                const int64_t r = SKEW ? st - K - 1 - 2 * j : st - K - (j + 1);
+                if (r >= 0 && r < nrows) acc[j] += popc_words<D>(nx);
+            }
+            if (j == K - 1) {
+                if (st >= lag && st - lag < nrows) {
+                    if (owned) store_words<D>(orow + col, nx);
+                    orow += p.pitch;
+                }
+            } else if (SKEW) {
+                pend[j + 1] = nx;
+            } else {
+                nc = nx;
+            }
+        }
+    };
 
     // Prefetch ring: loads run P steps ahead of their use (deeper for small K, whose steps are
     // short and would otherwise expose HBM latency).
     constexpr int P = K >= 4 ? 4 : (K == 2 ? 8 : 16);
-    uint32_t buf[P];
+    Words<D> buf[P];
 #pragma unroll
     for (int u = 0; u < P; ++u) buf[u] = load_next();
     for (int64_t s = 0; s < nsteps; s += P) {
 #pragma unroll
         for (int u = 0; u < P; ++u) {
-            if (SKEW)
-                GOL_STEP_SKEW((u & 1), buf[u], s + u);
+            if (u & 1)
+                step(std::integral_constant<int, 1>{}, buf[u], s + u);
             else
-                GOL_STEP((u & 1), buf[u], s + u);
+                step(std::integral_constant<int, 0>{}, buf[u], s + u);
             buf[u] = load_next();
         }
     }
-#undef GOL_STEP
-#undef GOL_STEP_SKEW
 
     if (COUNT) {
 #pragma unroll
@@ -483,19 +519,40 @@ inline unsigned grid_for(int64_t n, int threads = 256, int64_t cap = 8192) {
     return (unsigned)g;
 }
 
-template <int K, bool SKEW, int XL>
+template <int K, bool SKEW, int D>
 hipError_t launch_stencil_k(const uint32_t *in, uint32_t *out, const StencilParams &p,
                             unsigned long long *slots, hipStream_t s) {
     const int64_t waves = p.nbands * (int64_t)p.nchunks;
     const unsigned blocks = (unsigned)((waves + 3) / 4);
     if (blocks == 0) return hipSuccess;
     if (slots)
-        hipLaunchKernelGGL((gol_stencil<K, true, SKEW, XL>), dim3(blocks), dim3(256), 0, s, in,
+        hipLaunchKernelGGL((gol_stencil<K, true, SKEW, D>), dim3(blocks), dim3(256), 0, s, in,
                            out, p, slots);
     else
-        hipLaunchKernelGGL((gol_stencil<K, false, SKEW, XL>), dim3(blocks), dim3(256), 0, s, in,
+        hipLaunchKernelGGL((gol_stencil<K, false, SKEW, D>), dim3(blocks), dim3(256), 0, s, in,
                            out, p, slots);
     return hipGetLastError();
+}
+
+template <int K>
+hipError_t launch_variant(int variant, const uint32_t *in, uint32_t *out, const StencilParams &p,
+                          unsigned long long *slots, hipStream_t s) {
+    switch (variant) {
+        case kVariantChain: return launch_stencil_k<K, false, 1>(in, out, p, slots, s);
+        case kVariantSkewD2: return launch_stencil_k<K, true, 2>(in, out, p, slots, s);
+        case kVariantChainD2: return launch_stencil_k<K, false, 2>(in, out, p, slots, s);
+        default: return launch_stencil_k<K, true, 1>(in, out, p, slots, s);
+    }
+}
+
+template <int K>
+const void *variant_fn(int variant) {
+    switch (variant) {
+        case kVariantChain: return (const void *)gol_stencil<K, false, false, 1>;
+        case kVariantSkewD2: return (const void *)gol_stencil<K, false, true, 2>;
+        case kVariantChainD2: return (const void *)gol_stencil<K, false, false, 2>;
+        default: return (const void *)gol_stencil<K, false, true, 1>;
+    }
 }
 
 }  // namespace
@@ -506,43 +563,28 @@ bool stencil_k_supported(int K) {
 
 hipError_t launch_stencil(int K, int variant, const uint32_t *in_row0, uint32_t *out_row0,
                           const StencilParams &p, unsigned long long *slots, hipStream_t s) {
-#define GOL_CASE(KK)                                                                   \
-    case KK:                                                                           \
-        return variant == kVariantChain                                                \
-                   ? launch_stencil_k<KK, false, 0>(in_row0, out_row0, p, slots, s)    \
-                   : variant == kVariantSkewLds                                        \
-                         ? launch_stencil_k<KK, true, 1>(in_row0, out_row0, p, slots, s) \
-                         : launch_stencil_k<KK, true, 0>(in_row0, out_row0, p, slots, s);
     switch (K) {
-        GOL_CASE(1)
-        GOL_CASE(2)
-        GOL_CASE(4)
-        GOL_CASE(8)
-        GOL_CASE(16)
-        GOL_CASE(32)
+        case 1: return launch_variant<1>(variant, in_row0, out_row0, p, slots, s);
+        case 2: return launch_variant<2>(variant, in_row0, out_row0, p, slots, s);
+        case 4: return launch_variant<4>(variant, in_row0, out_row0, p, slots, s);
+        case 8: return launch_variant<8>(variant, in_row0, out_row0, p, slots, s);
+        case 16: return launch_variant<16>(variant, in_row0, out_row0, p, slots, s);
+        case 32: return launch_variant<32>(variant, in_row0, out_row0, p, slots, s);
         default: return hipErrorInvalidValue;
     }
-#undef GOL_CASE
 }
 
 int stencil_waves_per_cu(int K, int variant) {
     const void *fn = nullptr;
-#define GOL_FN(KK)                                                                           \
-    case KK:                                                                                 \
-        fn = variant == kVariantChain      ? (const void *)gol_stencil<KK, false, false, 0>  \
-             : variant == kVariantSkewLds ? (const void *)gol_stencil<KK, false, true, 1>   \
-                                          : (const void *)gol_stencil<KK, false, true, 0>;  \
-        break;
     switch (K) {
-        GOL_FN(1)
-        GOL_FN(2)
-        GOL_FN(4)
-        GOL_FN(8)
-        GOL_FN(16)
-        GOL_FN(32)
+        case 1: fn = variant_fn<1>(variant); break;
+        case 2: fn = variant_fn<2>(variant); break;
+        case 4: fn = variant_fn<4>(variant); break;
+        case 8: fn = variant_fn<8>(variant); break;
+        case 16: fn = variant_fn<16>(variant); break;
+        case 32: fn = variant_fn<32>(variant); break;
         default: return 4;
     }
-#undef GOL_FN
     int blocks = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, 256, 0) != hipSuccess || blocks < 1)
         return 4;
