@@ -39,7 +39,7 @@ constexpr int kVariantChainD2 = 3;
 constexpr int kNumVariants = 4;
 inline int variant_words(int v) { return v >= kVariantSkewD2 ? 2 : 1; }
 
-// Launch the K-generation stencil (K in {1,2,4,8,16,32}). count_slots (nullable) receives
+// Launch the K-generation stencil (K in {1,2,4,6,8,12,16,32}). count_slots (nullable) receives
 // per-generation alive counts in kCountSlots slots per generation.
 hipError_t launch_stencil(int K, int variant, const uint32_t *in_row0, uint32_t *out_row0,
                           const StencilParams &p, unsigned long long *count_slots,

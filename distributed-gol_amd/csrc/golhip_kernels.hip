@@ -558,7 +558,7 @@ const void *variant_fn(int variant) {
 }  // namespace
 
 bool stencil_k_supported(int K) {
-    return K == 1 || K == 2 || K == 4 || K == 8 || K == 16 || K == 32;
+    return K == 1 || K == 2 || K == 4 || K == 6 || K == 8 || K == 12 || K == 16 || K == 32;
 }
 
 hipError_t launch_stencil(int K, int variant, const uint32_t *in_row0, uint32_t *out_row0,
@@ -567,6 +567,8 @@ hipError_t launch_stencil(int K, int variant, const uint32_t *in_row0, uint32_t 
         case 1: return launch_variant<1>(variant, in_row0, out_row0, p, slots, s);
         case 2: return launch_variant<2>(variant, in_row0, out_row0, p, slots, s);
         case 4: return launch_variant<4>(variant, in_row0, out_row0, p, slots, s);
+        case 6: return launch_variant<6>(variant, in_row0, out_row0, p, slots, s);
+        case 12: return launch_variant<12>(variant, in_row0, out_row0, p, slots, s);
         case 8: return launch_variant<8>(variant, in_row0, out_row0, p, slots, s);
         case 16: return launch_variant<16>(variant, in_row0, out_row0, p, slots, s);
         case 32: return launch_variant<32>(variant, in_row0, out_row0, p, slots, s);
@@ -580,6 +582,8 @@ int stencil_waves_per_cu(int K, int variant) {
         case 1: fn = variant_fn<1>(variant); break;
         case 2: fn = variant_fn<2>(variant); break;
         case 4: fn = variant_fn<4>(variant); break;
+        case 6: fn = variant_fn<6>(variant); break;
+        case 12: fn = variant_fn<12>(variant); break;
         case 8: fn = variant_fn<8>(variant); break;
         case 16: fn = variant_fn<16>(variant); break;
         case 32: fn = variant_fn<32>(variant); break;

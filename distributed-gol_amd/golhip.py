@@ -116,6 +116,43 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
     return L
 
 
+def parse_rle(text: str) -> np.ndarray:
+    """Run-length-encoded Life pattern (the standard .rle format) -> 0/255 uint8 (h, w)."""
+    lines = [ln.strip() for ln in text.splitlines() if ln.strip() and not ln.startswith("#")]
+    header, body = lines[0], "".join(lines[1:])
+    dims = dict(kv.split("=") for kv in header.replace(" ", "").split(",")[:2])
+    w, h = int(dims["x"]), int(dims["y"])
+    out = np.zeros((h, w), dtype=np.uint8)
+    x = y = 0
+    run = ""
+    for ch in body:
+        if ch.isdigit():
+            run += ch
+            continue
+        n = int(run) if run else 1
+        run = ""
+        if ch == "b":
+            x += n
+        elif ch == "o":
+            out[y, x:x + n] = 255
+            x += n
+        elif ch == "$":
+            y += n
+            x = 0
+        elif ch == "!":
+            break
+    return out
+
+
+def place(board: np.ndarray, pattern: np.ndarray, x: int, y: int) -> None:
+    """Stamp a pattern at (x, y) on a torus board (in place)."""
+    h, w = pattern.shape
+    H, W = board.shape
+    ys = (np.arange(h) + y) % H
+    xs = (np.arange(w) + x) % W
+    board[np.ix_(ys, xs)] |= pattern
+
+
 def device_count() -> int:
     n = ctypes.c_int(0)
     load_library().golhip_device_count(ctypes.byref(n))

@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""Generate the golden vectors of the synthetic configs with the (pinned) CPU oracle.
+
+  cfg2: 5120x5120 random p=0.5 seed 2, per-turn alive counts for 10000 turns + final digest
+  cfg3: 65536x65536 random p=0.5 seed 3, per-turn counts for 1000 turns + digests at 8/1000
+  cfg5: 4096x4096 Gosper gun at (64,64) + R-pentomino at (2048,2048), counts for the first
+        100000 turns (SHA-256 of the uint32 array, every 1000th count listed)
+Digests = SHA-256 of the packed little-endian uint64 rows (oracle.digest_words).
+Run from the repo root: python scripts/make_golden.py [cfg2|cfg3|cfg5 ...]
+"""
+import hashlib
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "oracle"))
+sys.path.insert(0, str(ROOT / "distributed-gol_amd"))
+import oracle  # noqa: E402
+
+OUT = ROOT / "tests" / "golden"
+
+
+def cfg2():
+    w = oracle.init_random(5120, 5120, seed=2)
+    t = time.time()
+    counts = oracle.packed_run_words(w, 10000, threads=8)
+    (OUT / "cfg2_5120_seed2_counts.csv").write_text(
+        "completed_turns,alive_cells\n" + "".join(f"{i + 1},{c}\n" for i, c in enumerate(counts)))
+    return {"cfg2": {"width": 5120, "height": 5120, "seed": 2, "turns": 10000,
+                     "final_digest": oracle.digest_words(w), "counts_csv": "cfg2_5120_seed2_counts.csv",
+                     "oracle_seconds": round(time.time() - t, 1)}}
+
+
+def cfg3():
+    w = oracle.init_random(65536, 65536, seed=3)
+    t = time.time()
+    c8 = oracle.packed_run_words(w, 8, threads=8)
+    d8 = oracle.digest_words(w)
+    rest = oracle.packed_run_words(w, 992, threads=8)
+    counts = np.concatenate([c8, rest])
+    return {"cfg3": {"width": 65536, "height": 65536, "seed": 3, "turns": 1000,
+                     "digest_after_8": d8, "digest_after_1000": oracle.digest_words(w),
+                     "counts_sha256": hashlib.sha256(counts.astype("<u8").tobytes()).hexdigest(),
+                     "counts_every_50": {str(i + 1): int(counts[i]) for i in range(49, 1000, 50)},
+                     "count_after_1": int(counts[0]), "oracle_seconds": round(time.time() - t, 1)}}
+
+
+def cfg5_board():
+    import golhip
+
+    b = np.zeros((4096, 4096), dtype=np.uint8)
+    golhip.place(b, golhip.parse_rle((OUT / "gosper_gun.rle").read_text()), 64, 64)
+    golhip.place(b, golhip.parse_rle((OUT / "r_pentomino.rle").read_text()), 2048, 2048)
+    return b
+
+
+def cfg5():
+    b = cfg5_board()
+    w = oracle.pack(b)
+    t = time.time()
+    counts = oracle.packed_run_words(w, 100000, threads=8)
+    return {"cfg5": {"width": 4096, "height": 4096, "turns": 100000,
+                     "initial_alive": int((b == 255).sum()),
+                     "counts_u32_sha256": hashlib.sha256(counts.astype("<u4").tobytes()).hexdigest(),
+                     "counts_every_1000": {str(i + 1): int(counts[i]) for i in range(999, 100000, 1000)},
+                     "digest_after_100000": oracle.digest_words(w),
+                     "oracle_seconds": round(time.time() - t, 1)}}
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["cfg2", "cfg3", "cfg5"]
+    path = OUT / "synthetic_golden.json"
+    data = json.loads(path.read_text()) if path.exists() else {}
+    for name in which:
+        data.update(globals()[name]())
+        path.write_text(json.dumps(data, indent=1) + "\n")
+        print(name, "done", flush=True)

@@ -117,3 +117,17 @@ def test_init_random_definition(oracle):
     dens = oracle.init_random(64, 64, seed=3, density_q32=int(0.25 * 2**32))
     frac = np.unpackbits(dens.view(np.uint8)).mean()
     assert 0.2 < frac < 0.3
+
+
+def test_synthetic_golden_vectors_are_the_oracle(oracle):
+    """tests/golden/synthetic_golden.json came from scripts/make_golden.py: spot-check prefixes."""
+    import json
+
+    from conftest import GOLDEN
+
+    gold = json.loads((GOLDEN / "synthetic_golden.json").read_text())
+    expected = oracle.read_alive_csv(GOLDEN / gold["cfg2"]["counts_csv"])
+    w = oracle.init_random(5120, 5120, seed=2)
+    counts = oracle.packed_run_words(w, 20)
+    assert [int(c) for c in counts] == [expected[t] for t in range(1, 21)]
+    assert set(gold) >= {"cfg2", "cfg3", "cfg5"}
