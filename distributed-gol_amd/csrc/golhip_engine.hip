@@ -49,6 +49,16 @@ struct TimingPair {
     hipEvent_t a, b;
 };
 
+// A captured run of M K-generation blocks (small boards are launch-bound: one graph replay
+// replaces 2M launches).  Kernel arguments are baked in, so a graph is specific to the buffer
+// parity it starts from; M is even, so it ends on the parity it started from.
+struct GraphEntry {
+    int K = 0, M = 0, cur = 0;
+    bool counting = false;
+    int64_t band = 0;
+    hipGraphExec_t exec = nullptr;
+};
+
 }  // namespace
 
 struct golhip_engine {
@@ -65,6 +75,9 @@ struct golhip_engine {
     bool prev_valid = false;
     int64_t turn = 0;
     std::string err;
+    // graph replay of step blocks (single strip, small boards)
+    std::vector<GraphEntry> graphs;
+    unsigned long long *g_counts = nullptr;  // counts written by a counting graph
     // timing
     bool timing = false;
     std::vector<TimingPair> tpool;
@@ -79,6 +92,8 @@ struct golhip_engine {
 };
 
 namespace {
+
+thread_local std::string g_create_error;  // golhip_last_error(NULL): why the last create failed
 
 int fail(golhip_t h, int code, const char *fmt, ...) {
     if (h) {
@@ -513,6 +528,55 @@ int create_common(golhip_t h) {
     return GOLHIP_OK;
 }
 
+constexpr int kGraphGens = 128;  // generations per graph replay
+
+// Graphs pay off when a launch is short (launch-bound): < ~100 us of stencil work.
+bool graph_worthy(golhip_t h, int K) {
+    if (h->world_size != 1 || h->shards.size() != 1) return false;
+    if (const char *e = std::getenv("GOLHIP_GRAPHS")) return std::atoi(e) != 0;
+    return (double)h->L * (double)h->height * K <= 8e9;
+}
+
+int graph_for(golhip_t h, int K, int M, bool counting, hipGraphExec_t *out) {
+    Shard &s = h->shards[0];
+    const int64_t band = auto_band(h, s.rows, K);
+    for (auto &g : h->graphs)
+        if (g.K == K && g.M == M && g.cur == h->cur && g.counting == counting && g.band == band) {
+            *out = g.exec;
+            return GOLHIP_OK;
+        }
+    HIPCHK(h, hipSetDevice(s.device));
+    if (counting && !h->g_counts)
+        HIPCHK(h, hipMalloc(&h->g_counts, sizeof(unsigned long long) * kGraphGens * 2));
+    hipGraph_t graph = nullptr;
+    HIPCHK(h, hipStreamBeginCapture(s.compute, hipStreamCaptureModeThreadLocal));
+    hipError_t err = hipSuccess;
+    for (int i = 0; i < M && err == hipSuccess; ++i) {
+        const int c = h->cur ^ (i & 1);
+        StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0);
+        err = golhip::launch_stencil(K, h->variant, h->row0(s, c), h->row0(s, c ^ 1), p,
+                                     counting ? s.slots : nullptr, s.compute);
+        if (err == hipSuccess && counting)
+            err = golhip::launch_count_finalize(K, s.slots, h->g_counts + (int64_t)i * K,
+                                                s.compute);
+    }
+    hipError_t e2 = hipStreamEndCapture(s.compute, &graph);
+    if (err != hipSuccess || e2 != hipSuccess)
+        return fail(h, GOLHIP_ERR_HIP, "graph capture: %s", hipGetErrorString(err ? err : e2));
+    GraphEntry g;
+    g.K = K;
+    g.M = M;
+    g.cur = h->cur;
+    g.counting = counting;
+    g.band = band;
+    err = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (err != hipSuccess) return fail(h, GOLHIP_ERR_HIP, "graph instantiate: %s", hipGetErrorString(err));
+    h->graphs.push_back(g);
+    *out = g.exec;
+    return GOLHIP_OK;
+}
+
 }  // namespace
 
 // ================================================================================ C ABI ====
@@ -604,6 +668,7 @@ int golhip_create_strips(int width, int height, int nstrips, int ndevices, int k
     *out = h;
     return GOLHIP_OK;
 fail:
+    g_create_error = h->err.empty() ? golhip_strerror(rc) : h->err;
     for (auto &s : h->shards) free_shard(s);
     delete h;
     return rc;
@@ -637,14 +702,17 @@ int golhip_create_rank(int width, int height, int rank, int world_size, int devi
         ncclUniqueId id;
         std::memcpy(&id, nccl_id, sizeof id);
         (void)hipSetDevice(device);
-        if (ncclCommInitRank(&s.comm_nccl, world_size, id, rank) != ncclSuccess) {
-            rc = GOLHIP_ERR_RCCL;
+        const ncclResult_t nr = ncclCommInitRank(&s.comm_nccl, world_size, id, rank);
+        if (nr != ncclSuccess) {
+            rc = fail(h, GOLHIP_ERR_RCCL, "ncclCommInitRank(rank %d of %d, device %d): %s", rank,
+                      world_size, device, ncclGetErrorString(nr));
             goto fail;
         }
     }
     *out = h;
     return GOLHIP_OK;
 fail:
+    g_create_error = h->err.empty() ? golhip_strerror(rc) : h->err;
     for (auto &sh : h->shards) free_shard(sh);
     delete h;
     return rc;
@@ -652,6 +720,8 @@ fail:
 
 int golhip_destroy(golhip_t h) {
     if (!h) return GOLHIP_ERR_ARG;
+    for (auto &g : h->graphs) (void)hipGraphExecDestroy(g.exec);
+    if (h->g_counts) (void)hipFree(h->g_counts);
     for (auto &tp : h->tpool) {
         (void)hipEventDestroy(tp.a);
         (void)hipEventDestroy(tp.b);
@@ -661,7 +731,7 @@ int golhip_destroy(golhip_t h) {
     return GOLHIP_OK;
 }
 
-const char *golhip_last_error(golhip_t h) { return h ? h->err.c_str() : "null handle"; }
+const char *golhip_last_error(golhip_t h) { return h ? h->err.c_str() : g_create_error.c_str(); }
 
 int golhip_get_info(golhip_t h, golhip_info *out) {
     if (!h || !out) return GOLHIP_ERR_ARG;
@@ -783,8 +853,30 @@ int golhip_step(golhip_t h, int64_t turns, uint64_t *alive_per_turn) {
         if (rc) return rc;
     }
     int64_t done = 0;
+    const int Kfull = pick_k(h->k);
+    const int M = std::max(2, (kGraphGens / Kfull) & ~1);
+    const bool graphs = graph_worthy(h, Kfull) && turns >= (int64_t)M * Kfull;
     while (done < turns) {
         const int64_t left = turns - done;
+        if (graphs && left >= (int64_t)M * Kfull) {
+            hipGraphExec_t exec = nullptr;
+            int rc = graph_for(h, Kfull, M, counting, &exec);
+            if (rc) return rc;
+            Shard &s = h->shards[0];
+            HIPCHK(h, hipGraphLaunch(exec, s.compute));
+            if (counting)
+                HIPCHK(h, hipMemcpyAsync(s.d_counts + done, h->g_counts,
+                                         sizeof(unsigned long long) * (size_t)M * Kfull,
+                                         hipMemcpyDeviceToDevice, s.compute));
+            done += (int64_t)M * Kfull;
+            h->turn += (int64_t)M * Kfull;
+            h->prev_valid = (Kfull == 1);
+            if (h->timing) {
+                h->tlaunches += M;
+                h->tgens += (int64_t)M * Kfull;
+            }
+            continue;
+        }
         const int K = pick_k((int)std::min<int64_t>(left, h->k));
         int rc = step_block(h, K, counting ? done : -1);
         if (rc) return rc;

@@ -202,7 +202,8 @@ class Engine:
             rc = L.golhip_create_rank(width, height, rank, world_size, device, k, nccl_id,
                                       ctypes.byref(self._h))
         if rc != OK:
-            raise GolHipError(rc, L.golhip_strerror(rc).decode())
+            why = L.golhip_last_error(None).decode() or L.golhip_strerror(rc).decode()
+            raise GolHipError(rc, why)
         self.info = self.get_info()
 
     # -- plumbing

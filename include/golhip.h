@@ -99,7 +99,7 @@ int golhip_nccl_unique_id(uint8_t *out /* GOLHIP_NCCL_ID_BYTES */);
 int golhip_create_rank(int width, int height, int rank, int world_size, int device, int k,
                        const uint8_t *nccl_id, golhip_t *out);
 int golhip_destroy(golhip_t h);
-const char *golhip_last_error(golhip_t h);
+const char *golhip_last_error(golhip_t h);  /* h == NULL: why the last create failed (this thread) */
 int golhip_get_info(golhip_t h, golhip_info *out);
 
 /* ---- board in / out (gol/io.go:42-128, util/cell.go) ------------------------------------- */

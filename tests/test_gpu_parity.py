@@ -162,3 +162,24 @@ def test_row_strips_bytes_roundtrip(golhip, oracle):
         e.step(100)
         out = e.store()
     assert oracle.pgm_bytes(out) == (REF / "check/images/512x512x100.pgm").read_bytes()
+
+
+@pytest.mark.parametrize("k", [1, 8, 32])
+def test_graph_replay_matches_launches(golhip, oracle, monkeypatch, k):
+    """Small boards replay captured graphs of step blocks; both buffer parities, with and
+    without per-turn counts, must equal the oracle."""
+    w, h = 1000, 300
+    words = oracle.init_random(1024, h, seed=k)[:, :]
+    board = oracle.unpack(words, w)
+    monkeypatch.setenv("GOLHIP_GRAPHS", "1")
+    with golhip.Engine(w, h, k=k) as e:
+        e.load(board)
+        e.step(1)                                  # odd parity before the graphs
+        c1 = e.step(300, counts=True)              # graph replays + tail blocks
+        e.step(257)                                # graphs without counts
+        got = e.store()
+        cells = e.alive_cells()
+    exp, exp_counts = oracle.packed_run(board, 1 + 300 + 257)
+    assert np.array_equal(got, exp)
+    assert np.array_equal(c1.astype(np.int64), exp_counts[1:301])
+    assert len(cells) == int((exp == 255).sum())
