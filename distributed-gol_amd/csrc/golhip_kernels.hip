@@ -125,6 +125,34 @@ __device__ __forceinline__ Words<D> load_words(const uint32_t *p) {
     return v;
 }
 
+// Raw buffer store of a lane's D words: an offset past the descriptor's range is dropped by the
+// hardware, which is how halo lanes and pipeline-fill steps skip their store WITHOUT a branch
+// (a branch around the store would make the waitcnt pass count conservatively and shorten the
+// load prefetch distance).
+constexpr uint32_t kBufferRsrcWord3 = 0x00020000;  // gfx9-family raw buffer, 32-bit dwords
+constexpr int kOutOfRange = 0x40000000;
+template <int D>
+__device__ __forceinline__ void buffer_store_words(__amdgpu_buffer_rsrc_t r, int off,
+                                                   const Words<D> &v) {
+    if constexpr (D == 2) {
+        typedef int v2i __attribute__((ext_vector_type(2)));
+        v2i x = {(int)v.w[0], (int)v.w[1]};
+        __builtin_amdgcn_raw_buffer_store_b64(x, r, off, 0, 0);
+    } else {
+        __builtin_amdgcn_raw_buffer_store_b32((int)v.w[0], r, off, 0, 0);
+    }
+}
+
+// A copy the register allocator cannot coalesce away: moving a consumed ring slot into a fresh
+// register lets the refill load of that slot target the same register every iteration.
+template <int D>
+__device__ __forceinline__ Words<D> opaque_copy(const Words<D> &v) {
+    Words<D> r;
+#pragma unroll
+    for (int d = 0; d < D; ++d) asm volatile("v_mov_b32 %0, %1" : "=v"(r.w[d]) : "v"(v.w[d]));
+    return r;
+}
+
 template <int D>
 __device__ __forceinline__ void store_words(uint32_t *p, const Words<D> &v) {
     if constexpr (D == 2)
@@ -149,13 +177,15 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
     const int64_t chunk = wave % p.nchunks;
     const int64_t bandi = wave / p.nchunks;
     if (bandi >= p.nbands) return;  // wave-uniform
-    int64_t ya, yb;
+    // Row indices fit in 32 bits; keeping every loop-carried counter 32-bit keeps the compares
+    // on the SALU (gfx9 has no 64-bit signed s_cmp, a 64-bit compare would drag them into VGPRs).
+    int ya, yb;
     if (bandi < p.nbands0) {
-        ya = p.r0b + bandi * p.band;
-        yb = min(ya + p.band, p.r0e);
+        ya = (int)(p.r0b + bandi * p.band);
+        yb = (int)min((int64_t)ya + p.band, p.r0e);
     } else {
-        ya = p.r1b + (bandi - p.nbands0) * p.band;
-        yb = min(ya + p.band, p.r1e);
+        ya = (int)(p.r1b + (bandi - p.nbands0) * p.band);
+        yb = (int)min((int64_t)ya + p.band, p.r1e);
     }
     // lanes 1..62 own D words each; lanes 0 and 63 are the horizontal halo
     const int colraw = ((int)chunk * 62 + lane - 1) * D;
@@ -164,30 +194,27 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
 
     // Input row stream: rows ya-K, ya-K+1, ... (wrap mod H, or clamped to the halo'd strip).
     // Row pointers are wave-uniform (SGPRs); the lane adds its column.
-    int64_t ly = ya - K;
-    if (p.wrap_rows > 0) {
-        ly %= p.wrap_rows;
-        if (ly < 0) ly += p.wrap_rows;
+    const int wrap = (int)p.wrap_rows, lo = (int)p.lo, hi = (int)p.hi;
+    int ly = ya - K;
+    if (wrap > 0) {
+        ly %= wrap;
+        if (ly < 0) ly += wrap;
     } else {
-        ly = ly < p.lo ? p.lo : (ly >= p.hi ? p.hi - 1 : ly);
+        ly = ly < lo ? lo : (ly >= hi ? hi - 1 : ly);
     }
-    const uint32_t *lrow = in + ly * p.pitch;
+    // Next-row arithmetic is branch-free (scalar selects), so the waitcnt pass sees one straight
+    // line of loads and stores and keeps the full prefetch distance.
     auto load_next = [&]() -> Words<D> {
-        const Words<D> v = load_words<D>(lrow + col);
-        if (p.wrap_rows > 0) {
-            if (++ly == p.wrap_rows) {
-                ly = 0;
-                lrow = in;
-            } else {
-                lrow += p.pitch;
-            }
-        } else if (ly + 1 < p.hi) {
-            ++ly;
-            lrow += p.pitch;
-        }
+        const Words<D> v = load_words<D>(in + (int64_t)ly * p.pitch + col);
+        const int nx = ly + 1;
+        ly = wrap > 0 ? (nx == wrap ? 0 : nx) : (nx < hi ? nx : hi - 1);
         return v;
     };
-    uint32_t *orow = out + ya * p.pitch;
+    // Output: one raw-buffer descriptor over the band's rows (offsets stay 32-bit for any board).
+    const int rowbytes = (int)(p.pitch * 4);
+    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+        out + (int64_t)ya * p.pitch, 0, (yb - ya) * rowbytes, kBufferRsrcWord3);
+    const int lane_off = owned ? col * 4 : kOutOfRange;
 
     // Per level: a two-slot ring (X/Y swap roles every step) and, skewed, the pending input row.
     RowState<D> X[K], Y[K];
@@ -203,9 +230,9 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
         }
         acc[j] = 0;
     }
-    const int64_t nrows = yb - ya;
-    const int64_t lag = SKEW ? 3 * K - 1 : 2 * K;  // steps before the first stored row
-    const int64_t nsteps = nrows + lag;
+    const int nrows = yb - ya;
+    const int lag = SKEW ? 3 * K - 1 : 2 * K;  // steps before the first stored row
+    const int nsteps = nrows + lag;
 
     // One step: a new level-0 row enters, every level emits one row, the level-K row is stored.
     // PAR 0: above = X, mid = Y, new -> X.  PAR 1: above = Y, mid = X, new -> Y.
@@ -214,7 +241,7 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
     // Skewed: levels in descending order, level j takes pend[j] (level j-1's output of the
     //   previous step) and its output overwrites pend[j+1] after level j+1 has read it; level j's
     //   output row is ya - K + st - 1 - 2j.
-    auto step = [&](auto par, const Words<D> &vin, int64_t st) {
+    auto step = [&](auto par, const Words<D> &vin, int st) {
         constexpr int PAR = decltype(par)::value;
         Words<D> nc = vin;
 #pragma unroll
@@ -227,14 +254,14 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
             else
                 level_update<D>(Y[j], X[j], lin, nx);
             if (COUNT) {
-                const int64_t r = SKEW ? st - K - 1 - 2 * j : st - K - (j + 1);
+                const int r = SKEW ? st - K - 1 - 2 * j : st - K - (j + 1);
                 if (r >= 0 && r < nrows) acc[j] += popc_words<D>(nx);
             }
             if (j == K - 1) {
-                if (st >= lag && st - lag < nrows) {
-                    if (owned) store_words<D>(orow + col, nx);
-                    orow += p.pitch;
-                }
+                const int r = st - lag;  // stored row - ya
+                buffer_store_words<D>(orsrc,
+                                      lane_off + ((r >= 0 && r < nrows) ? r * rowbytes : kOutOfRange),
+                                      nx);
             } else if (SKEW) {
                 pend[j + 1] = nx;
             } else {
@@ -249,14 +276,18 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
     Words<D> buf[P];
 #pragma unroll
     for (int u = 0; u < P; ++u) buf[u] = load_next();
-    for (int64_t s = 0; s < nsteps; s += P) {
+    for (int s = 0; s < nsteps; s += P) {
 #pragma unroll
         for (int u = 0; u < P; ++u) {
-            if (u & 1)
-                step(std::integral_constant<int, 1>{}, buf[u], s + u);
-            else
-                step(std::integral_constant<int, 0>{}, buf[u], s + u);
+            // take the row out of the ring before refilling the slot, so the refill can issue
+            // into the same register every iteration (no loop-carried moves of in-flight loads,
+            // which would force a full vmcnt(0) drain)
+            const Words<D> vin = buf[u];
             buf[u] = load_next();
+            if (u & 1)
+                step(std::integral_constant<int, 1>{}, vin, s + u);
+            else
+                step(std::integral_constant<int, 0>{}, vin, s + u);
         }
     }
 
