@@ -201,6 +201,8 @@ int setup_engine(golhip_t h, int width, int height, int world, int k) {
         h->variant = std::strcmp(e, "chain") == 0     ? golhip::kVariantChain
                      : std::strcmp(e, "skew2") == 0  ? golhip::kVariantSkewD2
                      : std::strcmp(e, "chain2") == 0 ? golhip::kVariantChainD2
+                     : std::strcmp(e, "skewlds") == 0 ? golhip::kVariantSkewLdsPf
+                     : std::strcmp(e, "chainlds") == 0 ? golhip::kVariantChainLdsPf
                                                      : golhip::kVariantSkew;
     return GOLHIP_OK;
 }

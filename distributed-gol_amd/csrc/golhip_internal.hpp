@@ -36,8 +36,10 @@ constexpr int kVariantSkew = 0;
 constexpr int kVariantChain = 1;
 constexpr int kVariantSkewD2 = 2;
 constexpr int kVariantChainD2 = 3;
-constexpr int kNumVariants = 4;
-inline int variant_words(int v) { return v >= kVariantSkewD2 ? 2 : 1; }
+constexpr int kVariantSkewLdsPf = 4;   // input rows prefetched by LDS-DMA instead of VGPRs
+constexpr int kVariantChainLdsPf = 5;
+constexpr int kNumVariants = 6;
+inline int variant_words(int v) { return (v == kVariantSkewD2 || v == kVariantChainD2) ? 2 : 1; }
 
 // Launch the K-generation stencil (K in {1,2,4,6,8,12,16,32}). count_slots (nullable) receives
 // per-generation alive counts in kCountSlots slots per generation.

@@ -166,7 +166,7 @@ __device__ __forceinline__ void store_words(uint32_t *p, const Words<D> &v) {
 //               level j produced in the same step).
 // SKEW = true : level j consumes the row level j-1 produced in the PREVIOUS step, so the K level
 //               updates of a step are independent (K-way ILP); the pipeline is K-1 steps deeper.
-template <int K, bool COUNT, bool SKEW, int D>
+template <int K, bool COUNT, bool SKEW, int D, int PF>
 __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ in,
                                                    uint32_t *__restrict__ out, StencilParams p,
                                                    unsigned long long *__restrict__ slots) {
@@ -270,24 +270,59 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
         }
     };
 
-    // Prefetch ring: loads run P steps ahead of their use (deeper for small K, whose steps are
-    // short and would otherwise expose HBM latency).
-    constexpr int P = K >= 4 ? 4 : (K == 2 ? 8 : 16);
-    Words<D> buf[P];
+    if constexpr (PF == 0) {
+        // Register prefetch ring: loads run P steps ahead of their use (deeper for small K,
+        // whose steps are short and would otherwise expose HBM latency).
+        constexpr int P = K >= 4 ? 4 : (K == 2 ? 8 : 16);
+        Words<D> buf[P];
 #pragma unroll
-    for (int u = 0; u < P; ++u) buf[u] = load_next();
-    for (int s = 0; s < nsteps; s += P) {
+        for (int u = 0; u < P; ++u) buf[u] = load_next();
+        for (int s = 0; s < nsteps; s += P) {
 #pragma unroll
-        for (int u = 0; u < P; ++u) {
-            // take the row out of the ring before refilling the slot, so the refill can issue
-            // into the same register every iteration (no loop-carried moves of in-flight loads,
-            // which would force a full vmcnt(0) drain)
-            const Words<D> vin = buf[u];
-            buf[u] = load_next();
-            if (u & 1)
-                step(std::integral_constant<int, 1>{}, vin, s + u);
-            else
-                step(std::integral_constant<int, 0>{}, vin, s + u);
+            for (int u = 0; u < P; ++u) {
+                const Words<D> vin = buf[u];
+                buf[u] = load_next();
+                if (u & 1)
+                    step(std::integral_constant<int, 1>{}, vin, s + u);
+                else
+                    step(std::integral_constant<int, 0>{}, vin, s + u);
+            }
+        }
+    } else {
+        // LDS ring filled by LDS-DMA (global_load_lds): no VGPR destination, so the prefetch
+        // distance costs no registers and no register moves.  Each step waits (by hand: the
+        // compiler does not track LDS-DMA completion) until its row's DMA has landed: after
+        // DMA(t) this wave issued store(t-PL) and (DMA, store) for PL-1 steps, 2PL-1 younger
+        // VMEM ops; vmcnt(2PL-3) leaves a margin of two.
+        static_assert(D == 1, "LDS-DMA ring moves 4-byte words");
+        constexpr int PL = 8;
+        __shared__ uint32_t ring[4][PL][64];
+        const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+        auto dma_next = [&](int slot) {
+            __builtin_amdgcn_global_load_lds(in + (int64_t)ly * p.pitch + col, &ring[w][slot][0],
+                                             4, 0, 0);
+            const int nx = ly + 1;
+            ly = wrap > 0 ? (nx == wrap ? 0 : nx) : (nx < hi ? nx : hi - 1);
+        };
+        Words<D> zero;
+        zero.w[0] = 0;
+#pragma unroll
+        for (int u = 0; u < PL; ++u) {
+            dma_next(u);
+            buffer_store_words<D>(orsrc, kOutOfRange, zero);  // keeps the (DMA, store) cadence
+        }
+        for (int s = 0; s < nsteps; s += PL) {
+#pragma unroll
+            for (int u = 0; u < PL; ++u) {
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PL - 3) : "memory");
+                Words<D> vin;
+                vin.w[0] = ring[w][u][lane];
+                dma_next(u);
+                if (u & 1)
+                    step(std::integral_constant<int, 1>{}, vin, s + u);
+                else
+                    step(std::integral_constant<int, 0>{}, vin, s + u);
+            }
         }
     }
 
@@ -550,18 +585,18 @@ inline unsigned grid_for(int64_t n, int threads = 256, int64_t cap = 8192) {
     return (unsigned)g;
 }
 
-template <int K, bool SKEW, int D>
+template <int K, bool SKEW, int D, int PF = 0>
 hipError_t launch_stencil_k(const uint32_t *in, uint32_t *out, const StencilParams &p,
                             unsigned long long *slots, hipStream_t s) {
     const int64_t waves = p.nbands * (int64_t)p.nchunks;
     const unsigned blocks = (unsigned)((waves + 3) / 4);
     if (blocks == 0) return hipSuccess;
     if (slots)
-        hipLaunchKernelGGL((gol_stencil<K, true, SKEW, D>), dim3(blocks), dim3(256), 0, s, in,
-                           out, p, slots);
+        hipLaunchKernelGGL((gol_stencil<K, true, SKEW, D, PF>), dim3(blocks), dim3(256), 0, s,
+                           in, out, p, slots);
     else
-        hipLaunchKernelGGL((gol_stencil<K, false, SKEW, D>), dim3(blocks), dim3(256), 0, s, in,
-                           out, p, slots);
+        hipLaunchKernelGGL((gol_stencil<K, false, SKEW, D, PF>), dim3(blocks), dim3(256), 0, s,
+                           in, out, p, slots);
     return hipGetLastError();
 }
 
@@ -572,6 +607,8 @@ hipError_t launch_variant(int variant, const uint32_t *in, uint32_t *out, const 
         case kVariantChain: return launch_stencil_k<K, false, 1>(in, out, p, slots, s);
         case kVariantSkewD2: return launch_stencil_k<K, true, 2>(in, out, p, slots, s);
         case kVariantChainD2: return launch_stencil_k<K, false, 2>(in, out, p, slots, s);
+        case kVariantSkewLdsPf: return launch_stencil_k<K, true, 1, 1>(in, out, p, slots, s);
+        case kVariantChainLdsPf: return launch_stencil_k<K, false, 1, 1>(in, out, p, slots, s);
         default: return launch_stencil_k<K, true, 1>(in, out, p, slots, s);
     }
 }
@@ -579,10 +616,12 @@ hipError_t launch_variant(int variant, const uint32_t *in, uint32_t *out, const 
 template <int K>
 const void *variant_fn(int variant) {
     switch (variant) {
-        case kVariantChain: return (const void *)gol_stencil<K, false, false, 1>;
-        case kVariantSkewD2: return (const void *)gol_stencil<K, false, true, 2>;
-        case kVariantChainD2: return (const void *)gol_stencil<K, false, false, 2>;
-        default: return (const void *)gol_stencil<K, false, true, 1>;
+        case kVariantChain: return (const void *)gol_stencil<K, false, false, 1, 0>;
+        case kVariantSkewD2: return (const void *)gol_stencil<K, false, true, 2, 0>;
+        case kVariantChainD2: return (const void *)gol_stencil<K, false, false, 2, 0>;
+        case kVariantSkewLdsPf: return (const void *)gol_stencil<K, false, true, 1, 1>;
+        case kVariantChainLdsPf: return (const void *)gol_stencil<K, false, false, 1, 1>;
+        default: return (const void *)gol_stencil<K, false, true, 1, 0>;
     }
 }
 
