@@ -324,6 +324,9 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
                     step(std::integral_constant<int, 0>{}, vin, s + u);
             }
         }
+        // Drain the ring's in-flight DMAs before the wave can retire: a DMA landing after the
+        // workgroup released its LDS would write into the next workgroup's ring.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
 
     if (COUNT) {
