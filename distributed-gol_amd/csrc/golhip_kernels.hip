@@ -262,6 +262,7 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
                 buffer_store_words<D>(orsrc,
                                       lane_off + ((r >= 0 && r < nrows) ? r * rowbytes : kOutOfRange),
                                       nx);
+                if (PF) asm volatile("" ::: "memory");
             } else if (SKEW) {
                 pend[j + 1] = nx;
             } else {
@@ -298,9 +299,12 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
         constexpr int PL = 8;
         __shared__ uint32_t ring[4][PL][64];
         const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+        // Compiler-level fences (empty asm with a memory clobber) keep every DMA and store in
+        // program order, so the per-step vmcnt accounting holds whatever the scheduler does.
         auto dma_next = [&](int slot) {
             __builtin_amdgcn_global_load_lds(in + (int64_t)ly * p.pitch + col, &ring[w][slot][0],
                                              4, 0, 0);
+            asm volatile("" ::: "memory");
             const int nx = ly + 1;
             ly = wrap > 0 ? (nx == wrap ? 0 : nx) : (nx < hi ? nx : hi - 1);
         };
@@ -309,7 +313,10 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
 #pragma unroll
         for (int u = 0; u < PL; ++u) {
             dma_next(u);
-            buffer_store_words<D>(orsrc, kOutOfRange, zero);  // keeps the (DMA, store) cadence
+            // dummy (dropped) store keeps the (DMA, store) cadence; distinct offsets so no
+            // dead-store elimination merges them
+            buffer_store_words<D>(orsrc, kOutOfRange + 4 * u, zero);
+            asm volatile("" ::: "memory");
         }
         for (int s = 0; s < nsteps; s += PL) {
 #pragma unroll
