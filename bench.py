@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--size", type=int, default=65536, help="board width")
     ap.add_argument("--height", type=int, default=0,
                     help="total board height (default: size * N, weak scaling)")
-    ap.add_argument("--k", type=int, default=8, help="generations per stencil launch")
+    ap.add_argument("--k", type=int, default=16, help="generations per stencil launch")
     ap.add_argument("--band-rows", type=int, default=0)
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")

@@ -66,7 +66,7 @@ struct golhip_engine {
     int32_t wd = 0;
     int world_size = 1;
     int k = 1, halo = 0, band_rows = 0;
-    int variant = golhip::kVariantSkew;
+    int variant = golhip::kVariantChainLdsPf;  // fastest measured (profiles/r01_tune_*)
     int cus = 0;                 // compute units of the first device (grid sizing)
     int waves_per_cu[golhip::kMaxK + 1][golhip::kNumVariants] = {};  // occupancy cache per (K, variant)
     bool rank_mode = false;
@@ -199,11 +199,11 @@ int setup_engine(golhip_t h, int width, int height, int world, int k) {
     if (const char *e = std::getenv("GOLHIP_BAND_ROWS")) h->band_rows = std::atoi(e);
     if (const char *e = std::getenv("GOLHIP_VARIANT"))
         h->variant = std::strcmp(e, "chain") == 0     ? golhip::kVariantChain
+                     : std::strcmp(e, "skew") == 0   ? golhip::kVariantSkew
                      : std::strcmp(e, "skew2") == 0  ? golhip::kVariantSkewD2
                      : std::strcmp(e, "chain2") == 0 ? golhip::kVariantChainD2
                      : std::strcmp(e, "skewlds") == 0 ? golhip::kVariantSkewLdsPf
-                     : std::strcmp(e, "chainlds") == 0 ? golhip::kVariantChainLdsPf
-                                                     : golhip::kVariantSkew;
+                                                     : golhip::kVariantChainLdsPf;
     return GOLHIP_OK;
 }
 

@@ -183,3 +183,20 @@ def test_graph_replay_matches_launches(golhip, oracle, monkeypatch, k):
     assert np.array_equal(got, exp)
     assert np.array_equal(c1.astype(np.int64), exp_counts[1:301])
     assert len(cells) == int((exp == 255).sum())
+
+
+@pytest.mark.parametrize("variant", ["chainlds", "skewlds", "chain", "skew", "chain2", "skew2"])
+@pytest.mark.parametrize("k", [1, 6, 16])
+def test_every_kernel_variant(golhip, oracle, monkeypatch, variant, k):
+    """Every stencil variant (chained/skewed levels, 1 or 2 words per lane, register or LDS-DMA
+    prefetch) on the shapes that stress wrap, halo lanes and band seams."""
+    monkeypatch.setenv("GOLHIP_VARIANT", variant)
+    for (h, w) in [(77, 640), (16, 16), (300, 4160)]:
+        rng = np.random.default_rng(h + w + k)
+        board = ((rng.random((h, w)) < 0.4) * 255).astype(np.uint8)
+        turns = 2 * k + 1
+        exp, exp_counts = oracle.packed_run(board, turns)
+        for band in (0, 7):
+            out, counts, _, _ = run_engine(golhip, board, turns, k=k, counts=True, band_rows=band)
+            assert np.array_equal(out, exp), (variant, k, h, w, band)
+            assert np.array_equal(counts.astype(np.int64), exp_counts), (variant, k, h, w, band)
