@@ -70,6 +70,7 @@ struct golhip_engine {
     int cus = 0;                 // compute units of the first device (grid sizing)
     int waves_per_cu[golhip::kMaxK + 1][golhip::kNumVariants] = {};  // occupancy cache per (K, variant)
     bool rank_mode = false;
+    bool split = false;  // board held as halo'd row strips (world > 1, or GOLHIP_RING_SELF)
     std::vector<Shard> shards;
     int cur = 0;
     bool prev_valid = false;
@@ -195,7 +196,8 @@ int setup_engine(golhip_t h, int width, int height, int world, int k) {
     h->pitch = h->wd;
     h->world_size = world;
     h->k = k;
-    h->halo = world > 1 ? k : 0;
+    h->split = world > 1;
+    h->halo = h->split ? k : 0;
     if (const char *e = std::getenv("GOLHIP_BAND_ROWS")) h->band_rows = std::atoi(e);
     if (const char *e = std::getenv("GOLHIP_VARIANT"))
         h->variant = std::strcmp(e, "chain") == 0     ? golhip::kVariantChain
@@ -203,6 +205,8 @@ int setup_engine(golhip_t h, int width, int height, int world, int k) {
                      : std::strcmp(e, "skew2") == 0  ? golhip::kVariantSkewD2
                      : std::strcmp(e, "chain2") == 0 ? golhip::kVariantChainD2
                      : std::strcmp(e, "skewlds") == 0 ? golhip::kVariantSkewLdsPf
+                     : std::strcmp(e, "skewlds2") == 0 ? golhip::kVariantSkewLdsD2
+                     : std::strcmp(e, "chainlds2") == 0 ? golhip::kVariantChainLdsD2
                                                      : golhip::kVariantChainLdsPf;
     return GOLHIP_OK;
 }
@@ -253,7 +257,7 @@ StencilParams make_params(golhip_t h, const Shard &s, int K, int64_t r0b, int64_
     p.band = auto_band(h, std::max<int64_t>(total, 1), K);
     p.nbands0 = (r0e - r0b + p.band - 1) / p.band;
     p.nbands = p.nbands0 + (r1e - r1b + p.band - 1) / p.band;
-    p.wrap_rows = h->world_size == 1 ? h->height : 0;
+    p.wrap_rows = h->split ? 0 : h->height;
     p.lo = -(int64_t)h->halo;
     p.hi = s.rows + h->halo;
     p.wd = h->wd;
@@ -352,7 +356,7 @@ int exchange_halos(golhip_t h, int K) {
 
 // One K-generation block on every shard. counts_dev_off: index into s.d_counts (or -1).
 int step_block(golhip_t h, int K, int64_t counts_off) {
-    if (h->world_size > 1) {
+    if (h->split) {
         int rc = exchange_halos(h, K);
         if (rc) return rc;
     }
@@ -362,7 +366,7 @@ int step_block(golhip_t h, int K, int64_t counts_off) {
         unsigned long long *slots = counts_off >= 0 ? s.slots : nullptr;
         const uint32_t *in = h->row0(s, h->cur);
         uint32_t *out = h->row0(s, nxt);
-        if (h->world_size == 1) {
+        if (!h->split) {
             StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0);
             HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, p, slots, s.compute));
         } else if (s.rows >= 3 * K) {
@@ -403,7 +407,7 @@ int sync_all(golhip_t h) {
 // Sum n uint64 device values over every strip of the board into host memory `out`:
 // strips of this process are summed on the host, ranks with one ncclAllReduce.
 int reduce_u64(golhip_t h, const std::vector<unsigned long long *> &bufs, size_t n, uint64_t *out) {
-    if (h->rank_mode && h->world_size > 1) {
+    if (h->rank_mode && h->split) {
         Shard &s = h->shards[0];
         HIPCHK(h, hipSetDevice(s.device));
         NCCLCHK(h, ncclAllReduce(bufs[0], bufs[0], n, ncclUint64, ncclSum, s.comm_nccl,
@@ -534,7 +538,7 @@ constexpr int kGraphGens = 128;  // generations per graph replay
 
 // Graphs pay off when a launch is short (launch-bound): < ~100 us of stencil work.
 bool graph_worthy(golhip_t h, int K) {
-    if (h->world_size != 1 || h->shards.size() != 1) return false;
+    if (h->split || h->shards.size() != 1) return false;
     if (const char *e = std::getenv("GOLHIP_GRAPHS")) return std::atoi(e) != 0;
     return (double)h->L * (double)h->height * K <= 8e9;
 }
@@ -688,11 +692,21 @@ int golhip_create_rank(int width, int height, int rank, int world_size, int devi
     if (rc) return rc;
     if (rank < 0 || rank >= world_size || device < 0) return GOLHIP_ERR_ARG;
     if (world_size > 1 && !nccl_id) return GOLHIP_ERR_ARG;
+    const char *rs = std::getenv("GOLHIP_RING_SELF");
+    const bool ring_self = world_size == 1 && rs && std::atoi(rs) != 0;
+    if (ring_self && height < k) return GOLHIP_ERR_ARG;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) return GOLHIP_ERR_NODEV;
     golhip_t h = new golhip_engine();
     setup_engine(h, width, height, world_size, k);
     h->rank_mode = true;
+    // Test hook: GOLHIP_RING_SELF=1 makes a world-1 rank engine a ring of ONE halo'd strip whose
+    // halos go through RCCL send/recv to itself, so the whole rank-mode path (plan, RCCL group,
+    // interior/boundary overlap, count all-reduce) runs on a one-GPU box.
+    if (ring_self) {
+        h->split = true;
+        h->halo = k;
+    }
     h->shards.resize(1);
     Shard &s = h->shards[0];
     s.device = device;
@@ -700,9 +714,14 @@ int golhip_create_rank(int width, int height, int rank, int world_size, int devi
     strip_bounds(height, world_size, rank, s.y0, s.rows);
     if ((rc = check_device_arch(h, device))) goto fail;
     if ((rc = create_common(h))) goto fail;
-    if (world_size > 1) {
+    if (h->split) {
         ncclUniqueId id;
-        std::memcpy(&id, nccl_id, sizeof id);
+        if (nccl_id) {
+            std::memcpy(&id, nccl_id, sizeof id);
+        } else if (ncclGetUniqueId(&id) != ncclSuccess) {  // ring of one: a local id
+            rc = fail(h, GOLHIP_ERR_RCCL, "ncclGetUniqueId failed");
+            goto fail;
+        }
         (void)hipSetDevice(device);
         const ncclResult_t nr = ncclCommInitRank(&s.comm_nccl, world_size, id, rank);
         if (nr != ncclSuccess) {
@@ -950,7 +969,7 @@ int golhip_set_turn(golhip_t h, int64_t turn) {
 int golhip_set_k(golhip_t h, int k) {
     if (!h) return GOLHIP_ERR_ARG;
     if (k < 1 || k > golhip::kMaxK) return fail(h, GOLHIP_ERR_ARG, "k must be 1..%d", golhip::kMaxK);
-    if (h->world_size > 1 && k > h->halo)
+    if (h->split && k > h->halo)
         return fail(h, GOLHIP_ERR_ARG, "k=%d exceeds the %d halo rows allocated at create", k,
                     h->halo);
     h->k = k;

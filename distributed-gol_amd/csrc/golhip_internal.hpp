@@ -38,8 +38,15 @@ constexpr int kVariantSkewD2 = 2;
 constexpr int kVariantChainD2 = 3;
 constexpr int kVariantSkewLdsPf = 4;   // input rows prefetched by LDS-DMA instead of VGPRs
 constexpr int kVariantChainLdsPf = 5;
-constexpr int kNumVariants = 6;
-inline int variant_words(int v) { return (v == kVariantSkewD2 || v == kVariantChainD2) ? 2 : 1; }
+constexpr int kVariantSkewLdsD2 = 6;   // LDS-DMA ring, 2 words (64 cells) per lane
+constexpr int kVariantChainLdsD2 = 7;
+constexpr int kNumVariants = 8;
+inline int variant_words(int v) {
+    return (v == kVariantSkewD2 || v == kVariantChainD2 || v == kVariantSkewLdsD2 ||
+            v == kVariantChainLdsD2)
+               ? 2
+               : 1;
+}
 
 // Launch the K-generation stencil (K in {1,2,4,6,8,12,16,32}). count_slots (nullable) receives
 // per-generation alive counts in kCountSlots slots per generation.

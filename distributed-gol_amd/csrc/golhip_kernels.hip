@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
 #include <type_traits>
 
 #include "golhip_internal.hpp"
@@ -38,9 +39,9 @@ __device__ __forceinline__ uint32_t lane_from_east(uint32_t v) {  // lane i <- l
 #define GOL_BOP3(A, B, C, TT) __builtin_amdgcn_bitop3_b32((A), (B), (C), (TT))
 constexpr uint8_t kXor3 = GOL_TT(a ^ b ^ c);                          // 0x96
 constexpr uint8_t kMaj = GOL_TT((a & b) | (c & (a | b)));             // 0xE8
-constexpr uint8_t kTwosIs1 = GOL_TT((a ^ b) & ~c);                    // p, k, q -> T == 1
-constexpr uint8_t kTwosIs2 = GOL_TT((c & ~(a | b)) | (~c & a & b));   // p, k, q -> T == 2
-constexpr uint8_t kSelect = GOL_TT((a & b) | (~a & c));               // a ? b : c
+constexpr uint8_t kTwosEven = GOL_TT(~(a | b | c) | (~a & ~b & c) | (a & b & ~c));  // k,p,q
+constexpr uint8_t kOddSelect = GOL_TT((a & ~b) | (~a & c));                    // o ? !q : mc
+static_assert(kTwosEven == 0x43 && kOddSelect == 0x3a, "bitop3 truth tables");
 
 // D consecutive 32-bit words of one row held by one lane (D = 1 or 2).
 template <int D>
@@ -68,7 +69,11 @@ __device__ __forceinline__ void row_sum3(const Words<D> &c, Words<D> &s, Words<D
 
 // B3/S23 from three rows' 3-cell sums: S9 = 9-cell sum including the centre cell mc;
 // alive next iff S9 == 3, or S9 == 4 and the cell is alive (server/server.go:35-52).
-// 8 VALU ops per word (7 v_bitop3 + 1 v_and).
+// S9 = o + 2T with T = k + p + 2q (o,k: full adder of the sum bits, p,q: of the carries).
+//   o = 1: next iff T == 1, i.e. q = 0 and T != 0, 2;     o = 0: next iff mc and T in {0, 2}
+//   (T == 0 with mc alive cannot happen: mc is part of S9).
+// With u = [T in {0,2}] and v = o ? !q : mc this is next = v & (o ^ u): 7 v_bitop3 per word,
+// u and v independent (found by exhaustive search over 3-gate circuits on o,k,p,q,mc).
 __device__ __forceinline__ uint32_t life_next(uint32_t as, uint32_t acy, uint32_t ms,
                                               uint32_t mcy, uint32_t mc, uint32_t bs,
                                               uint32_t bcy) {
@@ -76,10 +81,9 @@ __device__ __forceinline__ uint32_t life_next(uint32_t as, uint32_t acy, uint32_
     const uint32_t k = GOL_BOP3(as, ms, bs, kMaj);     // carry into the twos
     const uint32_t p = GOL_BOP3(acy, mcy, bcy, kXor3);
     const uint32_t q = GOL_BOP3(acy, mcy, bcy, kMaj);
-    // T = S9 >> 1 = p + 2q + k
-    const uint32_t t1 = GOL_BOP3(p, k, q, kTwosIs1);   // T == 1  (S9 == 3 when o)
-    const uint32_t t2 = GOL_BOP3(p, k, q, kTwosIs2);   // T == 2  (S9 == 4 when !o)
-    return GOL_BOP3(o, t1, mc & t2, kSelect);
+    const uint32_t u = GOL_BOP3(k, p, q, kTwosEven);
+    const uint32_t v = GOL_BOP3(o, q, mc, kOddSelect);
+    return GOL_BOP3(v, o, u, GOL_TT(a & (b ^ c)));
 }
 
 // A row's per-level state: 3-cell sum, carry and the cells themselves.
@@ -291,39 +295,52 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
         }
     } else {
         // LDS ring filled by LDS-DMA (global_load_lds): no VGPR destination, so the prefetch
-        // distance costs no registers and no register moves.  Each step waits (by hand: the
-        // compiler does not track LDS-DMA completion) until its row's DMA has landed: after
-        // DMA(t) this wave issued store(t-PL) and (DMA, store) for PL-1 steps, 2PL-1 younger
-        // VMEM ops; vmcnt(2PL-3) leaves a margin of two.
-        static_assert(D == 1, "LDS-DMA ring moves 4-byte words");
+        // distance costs no registers and no register moves.  A row chunk is D DMAs of 64
+        // consecutive words (lane L of DMA i fetches word base + 64i + L), read back as the
+        // lane's D consecutive words.  Each step waits (by hand: the compiler does not track
+        // LDS-DMA completion) until its row's DMAs have landed: a step issues D DMAs and one
+        // store, so after the last DMA for step t this wave issued store(t-PL) and (D DMAs,
+        // store) for PL-1 steps, (D+1)(PL-1)+1 younger VMEM ops; the wait leaves a margin of 2.
         constexpr int PL = 8;
-        __shared__ uint32_t ring[4][PL][64];
+        constexpr int kWait = (D + 1) * (PL - 1) - 1;
+        __shared__ __attribute__((aligned(16))) uint32_t ring[4][PL][64 * D];
         const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+        int dcol[D];
+        {
+            const int base = ((int)chunk * 62 - 1) * D;
+#pragma unroll
+            for (int i = 0; i < D; ++i) dcol[i] = (base + 64 * i + lane + p.wd) % p.wd;
+        }
         // Compiler-level fences (empty asm with a memory clobber) keep every DMA and store in
         // program order, so the per-step vmcnt accounting holds whatever the scheduler does.
         auto dma_next = [&](int slot) {
-            __builtin_amdgcn_global_load_lds(in + (int64_t)ly * p.pitch + col, &ring[w][slot][0],
-                                             4, 0, 0);
-            asm volatile("" ::: "memory");
+            const uint32_t *row = in + (int64_t)ly * p.pitch;
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                __builtin_amdgcn_global_load_lds(row + dcol[i], &ring[w][slot][64 * i], 4, 0, 0);
+                asm volatile("" ::: "memory");
+            }
             const int nx = ly + 1;
             ly = wrap > 0 ? (nx == wrap ? 0 : nx) : (nx < hi ? nx : hi - 1);
         };
         Words<D> zero;
-        zero.w[0] = 0;
+#pragma unroll
+        for (int d = 0; d < D; ++d) zero.w[d] = 0;
 #pragma unroll
         for (int u = 0; u < PL; ++u) {
             dma_next(u);
             // dummy (dropped) store keeps the (DMA, store) cadence; distinct offsets so no
             // dead-store elimination merges them
-            buffer_store_words<D>(orsrc, kOutOfRange + 4 * u, zero);
+            buffer_store_words<D>(orsrc, kOutOfRange + 8 * u, zero);
             asm volatile("" ::: "memory");
         }
         for (int s = 0; s < nsteps; s += PL) {
 #pragma unroll
             for (int u = 0; u < PL; ++u) {
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PL - 3) : "memory");
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kWait) : "memory");
                 Words<D> vin;
-                vin.w[0] = ring[w][u][lane];
+#pragma unroll
+                for (int d = 0; d < D; ++d) vin.w[d] = ring[w][u][lane * D + d];
                 dma_next(u);
                 if (u & 1)
                     step(std::integral_constant<int, 1>{}, vin, s + u);
@@ -595,6 +612,16 @@ inline unsigned grid_for(int64_t n, int threads = 256, int64_t cap = 8192) {
     return (unsigned)g;
 }
 
+// Tuning knob (GOLHIP_LDS_PAD = bytes of unused dynamic LDS per block): caps the resident blocks
+// per CU, to measure the stencil's sensitivity to occupancy.  0 in production.
+inline size_t lds_pad_bytes() {
+    static const size_t pad = [] {
+        const char *e = std::getenv("GOLHIP_LDS_PAD");
+        return e ? (size_t)std::atol(e) : (size_t)0;
+    }();
+    return pad;
+}
+
 template <int K, bool SKEW, int D, int PF = 0>
 hipError_t launch_stencil_k(const uint32_t *in, uint32_t *out, const StencilParams &p,
                             unsigned long long *slots, hipStream_t s) {
@@ -602,11 +629,11 @@ hipError_t launch_stencil_k(const uint32_t *in, uint32_t *out, const StencilPara
     const unsigned blocks = (unsigned)((waves + 3) / 4);
     if (blocks == 0) return hipSuccess;
     if (slots)
-        hipLaunchKernelGGL((gol_stencil<K, true, SKEW, D, PF>), dim3(blocks), dim3(256), 0, s,
-                           in, out, p, slots);
+        hipLaunchKernelGGL((gol_stencil<K, true, SKEW, D, PF>), dim3(blocks), dim3(256),
+                           lds_pad_bytes(), s, in, out, p, slots);
     else
-        hipLaunchKernelGGL((gol_stencil<K, false, SKEW, D, PF>), dim3(blocks), dim3(256), 0, s,
-                           in, out, p, slots);
+        hipLaunchKernelGGL((gol_stencil<K, false, SKEW, D, PF>), dim3(blocks), dim3(256),
+                           lds_pad_bytes(), s, in, out, p, slots);
     return hipGetLastError();
 }
 
@@ -619,6 +646,8 @@ hipError_t launch_variant(int variant, const uint32_t *in, uint32_t *out, const 
         case kVariantChainD2: return launch_stencil_k<K, false, 2>(in, out, p, slots, s);
         case kVariantSkewLdsPf: return launch_stencil_k<K, true, 1, 1>(in, out, p, slots, s);
         case kVariantChainLdsPf: return launch_stencil_k<K, false, 1, 1>(in, out, p, slots, s);
+        case kVariantSkewLdsD2: return launch_stencil_k<K, true, 2, 1>(in, out, p, slots, s);
+        case kVariantChainLdsD2: return launch_stencil_k<K, false, 2, 1>(in, out, p, slots, s);
         default: return launch_stencil_k<K, true, 1>(in, out, p, slots, s);
     }
 }
@@ -631,6 +660,8 @@ const void *variant_fn(int variant) {
         case kVariantChainD2: return (const void *)gol_stencil<K, false, false, 2, 0>;
         case kVariantSkewLdsPf: return (const void *)gol_stencil<K, false, true, 1, 1>;
         case kVariantChainLdsPf: return (const void *)gol_stencil<K, false, false, 1, 1>;
+        case kVariantSkewLdsD2: return (const void *)gol_stencil<K, false, true, 2, 1>;
+        case kVariantChainLdsD2: return (const void *)gol_stencil<K, false, false, 2, 1>;
         default: return (const void *)gol_stencil<K, false, true, 1, 0>;
     }
 }
@@ -670,7 +701,7 @@ int stencil_waves_per_cu(int K, int variant) {
         default: return 4;
     }
     int blocks = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, 256, 0) != hipSuccess || blocks < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, 256, lds_pad_bytes()) != hipSuccess || blocks < 1)
         return 4;
     return blocks * 4;  // 256-thread blocks = 4 waves
 }

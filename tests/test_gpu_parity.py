@@ -154,6 +154,29 @@ def test_row_strips_with_halo_exchange(golhip, oracle, strips, k):
     assert [tuple(c) for c in flips.tolist()] == oracle.flips(board, oracle.unpack(ref2, w))
 
 
+@pytest.mark.parametrize("k", [1, 4, 16])
+def test_rank_mode_rccl_ring_of_one(golhip, oracle, monkeypatch, k):
+    """Rank mode (golhip_create_rank) as a ring of ONE halo'd strip (GOLHIP_RING_SELF test hook):
+    the halos go through ncclSend/ncclRecv to itself in one group on the comm stream, the
+    interior launch overlaps them, the boundary bands wait for them, and per-turn counts go
+    through ncclAllReduce -- the RCCL path bench.py --gpus N uses, on the box's one GPU."""
+    monkeypatch.setenv("GOLHIP_RING_SELF", "1")
+    w, h = 640, 5 * k + 37
+    words = oracle.init_random(w, h, seed=500 + k)
+    turns = 3 * k + 2
+    with golhip.Engine(w, h, k=k, rank=0, world_size=1, device=0) as e:
+        assert e.info.halo_rows == k and e.info.world_size == 1
+        e.load_words(words)
+        counts = e.step(turns, counts=True)
+        got = e.store_words()
+        n = e.alive_count()
+    ref = words.copy()
+    ref_counts = oracle.packed_run_words(ref, turns)
+    assert np.array_equal(got, ref)
+    assert np.array_equal(counts.astype(np.int64), ref_counts)
+    assert n == int(ref_counts[-1])
+
+
 def test_row_strips_bytes_roundtrip(golhip, oracle):
     _, _, board = oracle.read_pgm(REF / "images/512x512.pgm")
     with golhip.Engine(512, 512, ngpus=1, k=8, strips=4) as e:
@@ -185,7 +208,7 @@ def test_graph_replay_matches_launches(golhip, oracle, monkeypatch, k):
     assert len(cells) == int((exp == 255).sum())
 
 
-@pytest.mark.parametrize("variant", ["chainlds", "skewlds", "chain", "skew", "chain2", "skew2"])
+@pytest.mark.parametrize("variant", ["chainlds", "skewlds", "chainlds2", "skewlds2", "chain", "skew", "chain2", "skew2"])
 @pytest.mark.parametrize("k", [1, 6, 16])
 def test_every_kernel_variant(golhip, oracle, monkeypatch, variant, k):
     """Every stencil variant (chained/skewed levels, 1 or 2 words per lane, register or LDS-DMA
