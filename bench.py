@@ -137,6 +137,9 @@ def main():
     dt = timed_steps(eng, a.steps, world)
     kern_ms, launches, gens = eng.kernel_time()
     eng.timing(False)
+    # regression canary: alive cells after exactly warmup + steps generations (deterministic for
+    # the seed; compare across kernel versions)
+    alive_timed = eng.alive_count()
     if a.no_timing:
         launches = -(-a.steps // a.k)
         kern_ms, gens = dt * 1e3, a.steps
@@ -209,6 +212,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "k_sweep_gcups": sweep,
+            "alive_after_timed": int(alive_timed),
             "alive_after": int(checksum),
         }
         print(json.dumps(line), flush=True)

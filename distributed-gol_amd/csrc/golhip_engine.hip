@@ -222,13 +222,15 @@ int pick_k(int n) {
     return kk;
 }
 
-int64_t auto_band(golhip_t h, int64_t rows_total, int K) {
+// Rows per wave band of a stencil launch over rows_total rows.  reserve_waves: resident wave
+// slots to leave free for a concurrent launch (the boundary bands of a split board).
+int64_t auto_band(golhip_t h, int64_t rows_total, int K, int64_t reserve_waves = 0) {
     if (h->band_rows > 0) return h->band_rows;
-    const int64_t per = 62 * golhip::variant_words(h->variant);
+    const int64_t per = golhip::chunk_words(K, h->variant);
     const int64_t nchunks = (h->wd + per - 1) / per;
-    // Fill the chip exactly once: as many waves as can be resident (CUs x resident waves per CU)
-    // so every SIMD gets the same number of equal bands; a band is at least 2K rows (the
-    // pipeline fill of a K-level band is 2K..3K steps) and at most 1024.
+    // Fill the chip in whole rounds of resident waves (CUs x resident waves per CU), so every
+    // SIMD gets the same number of equal bands; a band is at least 2K rows (the pipeline fill of
+    // a K-level band is 2K..3K steps).
     if (h->cus == 0) {
         hipDeviceProp_t prop;
         h->cus = hipGetDeviceProperties(&prop, h->shards[0].device) == hipSuccess
@@ -238,10 +240,23 @@ int64_t auto_band(golhip_t h, int64_t rows_total, int K) {
     int &wpc = h->waves_per_cu[K][h->variant];
     if (wpc == 0) wpc = golhip::stencil_waves_per_cu(K, h->variant);
     const int64_t capacity = (int64_t)h->cus * wpc;
-    int64_t band = (rows_total * nchunks + capacity - 1) / capacity;
+    // Waves = bands x chunks.  At most `slots` bands are resident at once; use the fewest whole
+    // rounds of `slots` bands that keep a band <= kMaxBand rows and split the rows evenly over
+    // them.  (A band count just above a round would run its few extra waves after the first
+    // round: a tail as long as a whole band with the chip nearly idle.)
+    constexpr int64_t kMaxBand = 4096;
+    const int64_t slots = std::max<int64_t>(1, (capacity - reserve_waves) / nchunks);
+    const int64_t rounds = (rows_total + slots * kMaxBand - 1) / (slots * kMaxBand);
+    int64_t band = (rows_total + rounds * slots - 1) / (rounds * slots);
     band = std::max<int64_t>(band, std::min<int64_t>(2 * K, rows_total));
     band = std::max<int64_t>(band, 1);
-    band = std::min<int64_t>(band, 1024);
+    // A wave runs band + lag steps in blocks of 8 (the kernel's prefetch ring); round the band so
+    // that full bands end on a block boundary instead of computing up to 7 discarded rows.
+    const bool skew = h->variant == golhip::kVariantSkew || h->variant == golhip::kVariantSkewD2 ||
+                      h->variant == golhip::kVariantSkewLdsPf ||
+                      h->variant == golhip::kVariantSkewLdsD2;
+    const int64_t lag = skew ? 3 * K - 1 : 2 * K;
+    if (band < rows_total) band = std::max<int64_t>(8, (band + lag + 7) / 8 * 8 - lag);
     return band;
 }
 
@@ -261,7 +276,7 @@ StencilParams make_params(golhip_t h, const Shard &s, int K, int64_t r0b, int64_
     p.lo = -(int64_t)h->halo;
     p.hi = s.rows + h->halo;
     p.wd = h->wd;
-    const int per = 62 * golhip::variant_words(h->variant);
+    const int per = golhip::chunk_words(K, h->variant);
     p.nchunks = (h->wd + per - 1) / per;
     return p;
 }

@@ -47,6 +47,12 @@ inline int variant_words(int v) {
                ? 2
                : 1;
 }
+// Words of a row owned by one wave of the stencil (its column chunk): 62 lanes x D words, or 63
+// words with the half-word halo (D = 1, K <= 16: lanes 0 and 63 own half a word each).
+inline int chunk_words(int K, int variant) {
+    const int d = variant_words(variant);
+    return (d == 1 && K <= 16) ? 63 : 62 * d;
+}
 
 // Launch the K-generation stencil (K in {1,2,4,6,8,12,16,32}). count_slots (nullable) receives
 // per-generation alive counts in kCountSlots slots per generation.

@@ -20,6 +20,7 @@
 
 #include <cstdlib>
 #include <type_traits>
+#include <utility>
 
 #include "golhip_internal.hpp"
 
@@ -165,15 +166,34 @@ __device__ __forceinline__ void store_words(uint32_t *p, const Words<D> &v) {
         *p = v.w[0];
 }
 
+template <int... I, class F>
+__device__ __forceinline__ void static_for(std::integer_sequence<int, I...>, F &&f) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+
+// Level update without the rule: only ingests the new row's 3-cell sums into the ring (pipeline
+// fill: the level's output would be garbage, but the rows it holds are needed two steps later).
+template <int D>
+__device__ __forceinline__ void level_ingest(RowState<D> &above, const Words<D> &in) {
+    row_sum3<D>(in, above.s, above.cy);
+    above.c = in;
+}
+
+// Column geometry of a wave's 64 lanes (shared with the host via chunk_words()):
+//   default : lanes 1..62 own D words each, lanes 0 and 63 are the horizontal halo (K <= 32);
+//   HH      : (D = 1, K <= 16) a halo needs only K <= 16 bits, so lane 0 owns the upper and lane 63
+//             the lower half of its word: 63 words per wave, chunk c owns cells
+//             [2016c - 16, 2016(c+1) - 16) (unwrapped), stored as full words plus two halves.
 // The hot kernel.  K = generations per launch, D = words per lane.
 // SKEW = false: the K levels of one step form one dependent chain (level j+1 consumes the row
 //               level j produced in the same step).
 // SKEW = true : level j consumes the row level j-1 produced in the PREVIOUS step, so the K level
 //               updates of a step are independent (K-way ILP); the pipeline is K-1 steps deeper.
-template <int K, bool COUNT, bool SKEW, int D, int PF>
+template <int K, bool COUNT, bool SKEW, int D, int PF, bool HH>
 __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ in,
                                                    uint32_t *__restrict__ out, StencilParams p,
                                                    unsigned long long *__restrict__ slots) {
+    static_assert(!HH || (D == 1 && K <= 16), "half-word halo needs D = 1, K <= 16");
     const int lane = threadIdx.x & 63;
     // wave index made provably uniform so every band/row quantity lives in SGPRs
     const int64_t wave =
@@ -191,10 +211,10 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
         ya = (int)(p.r1b + (bandi - p.nbands0) * p.band);
         yb = (int)min((int64_t)ya + p.band, p.r1e);
     }
-    // lanes 1..62 own D words each; lanes 0 and 63 are the horizontal halo
-    const int colraw = ((int)chunk * 62 + lane - 1) * D;
+    // First word (unwrapped) of this lane and its wrapped column.
+    const int stride = HH ? 63 : 62 * D;
+    const int colraw = (int)chunk * stride + (lane - 1) * D;
     const int col = (colraw + p.wd) % p.wd;
-    const bool owned = lane >= 1 && lane <= 62 && colraw < p.wd;
 
     // Input row stream: rows ya-K, ya-K+1, ... (wrap mod H, or clamped to the halo'd strip).
     // Row pointers are wave-uniform (SGPRs); the lane adds its column.
@@ -215,10 +235,38 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
         return v;
     };
     // Output: one raw-buffer descriptor over the band's rows (offsets stay 32-bit for any board).
+    // Each lane stores through at most one of: a full store (off_full), the low half (off_lo) or
+    // the high half (off_hi, HH only); the others point past the descriptor and are dropped.
     const int rowbytes = (int)(p.pitch * 4);
     const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
         out + (int64_t)ya * p.pitch, 0, (yb - ya) * rowbytes, kBufferRsrcWord3);
-    const int lane_off = owned ? col * 4 : kOutOfRange;
+    int off_full = kOutOfRange, off_lo = kOutOfRange, off_hi = kOutOfRange;
+    uint32_t own_mask = 0;  // owned cells of the lane's (first) word, for the counts
+    if (HH) {
+        // owned unwrapped cells: [-16, 32wd - 16); lane 0 -> upper half, lane 63 -> lower half
+        const int last = p.wd - 1;
+        if (lane == 0) {
+            if (colraw <= last - 1) { off_hi = col * 4 + 2; own_mask = 0xffff0000u; }
+        } else if (lane == 63) {
+            if (colraw <= last) { off_lo = col * 4; own_mask = 0x0000ffffu; }
+        } else if (colraw < last) {
+            off_full = col * 4; own_mask = ~0u;
+        } else if (colraw == last) {
+            off_lo = col * 4; own_mask = 0x0000ffffu;
+        }
+    } else if (lane >= 1 && lane <= 62 && colraw < p.wd) {
+        off_full = col * 4;
+        own_mask = ~0u;
+    }
+    constexpr int NSTORE = HH ? 3 : 1;  // vector-memory stores per step
+    auto store_row = [&](const Words<D> &v, int rowoff) {
+        buffer_store_words<D>(orsrc, off_full + rowoff, v);
+        if (HH) {
+            __builtin_amdgcn_raw_buffer_store_b16((short)v.w[0], orsrc, off_lo + rowoff, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b16((short)(v.w[0] >> 16), orsrc, off_hi + rowoff, 0,
+                                                  0);
+        }
+    };
 
     // Per level: a two-slot ring (X/Y swap roles every step) and, skewed, the pending input row.
     RowState<D> X[K], Y[K];
@@ -241,17 +289,26 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
     // One step: a new level-0 row enters, every level emits one row, the level-K row is stored.
     // PAR 0: above = X, mid = Y, new -> X.  PAR 1: above = Y, mid = X, new -> Y.
     // Chained: level j+1 takes level j's output of this step; level j's output row is
-    //   ya - K + st - (j+1).
+    //   ya - K + st - (j+1), valid from step 2j+2 on (its above/mid rows arrive at steps 2j and
+    //   2j+1).  FILL = true (pipeline-fill steps only): level j is skipped before step 2j and only
+    //   ingests its input at steps 2j, 2j+1 -- the garbage rows of the fill are never computed.
     // Skewed: levels in descending order, level j takes pend[j] (level j-1's output of the
     //   previous step) and its output overwrites pend[j+1] after level j+1 has read it; level j's
     //   output row is ya - K + st - 1 - 2j.
-    auto step = [&](auto par, const Words<D> &vin, int st) {
+    auto step = [&](auto par, auto fill, const Words<D> &vin, int st) {
         constexpr int PAR = decltype(par)::value;
+        constexpr int FST = decltype(fill)::value;  // fill step index (compile time) or -1
+        constexpr bool FILL = FST >= 0 && !SKEW;
         Words<D> nc = vin;
 #pragma unroll
         for (int jj = 0; jj < K; ++jj) {
             const int j = SKEW ? K - 1 - jj : jj;
             const Words<D> lin = SKEW ? (j == 0 ? vin : pend[j]) : nc;
+            if (FILL && FST < 2 * j + 2) {  // folds away: FST and (unrolled) j are constants
+                if (FST >= 2 * j) level_ingest<D>(PAR == 0 ? X[j] : Y[j], lin);
+                if (j == K - 1) store_row(lin, kOutOfRange);  // keep the per-step store count
+                continue;
+            }
             Words<D> nx;
             if (PAR == 0)
                 level_update<D>(X[j], Y[j], lin, nx);
@@ -259,13 +316,12 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
                 level_update<D>(Y[j], X[j], lin, nx);
             if (COUNT) {
                 const int r = SKEW ? st - K - 1 - 2 * j : st - K - (j + 1);
-                if (r >= 0 && r < nrows) acc[j] += popc_words<D>(nx);
+                if (r >= 0 && r < nrows) acc[j] += __builtin_popcount(nx.w[0] & own_mask) +
+                                                   (D == 2 ? __builtin_popcount(nx.w[D - 1] & own_mask) : 0);
             }
             if (j == K - 1) {
                 const int r = st - lag;  // stored row - ya
-                buffer_store_words<D>(orsrc,
-                                      lane_off + ((r >= 0 && r < nrows) ? r * rowbytes : kOutOfRange),
-                                      nx);
+                store_row(nx, (r >= 0 && r < nrows) ? r * rowbytes : kOutOfRange);
                 if (PF) asm volatile("" ::: "memory");
             } else if (SKEW) {
                 pend[j + 1] = nx;
@@ -274,6 +330,9 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
             }
         }
     };
+    using Par0 = std::integral_constant<int, 0>;
+    using Par1 = std::integral_constant<int, 1>;
+    using Steady = std::integral_constant<int, -1>;
 
     if constexpr (PF == 0) {
         // Register prefetch ring: loads run P steps ahead of their use (deeper for small K,
@@ -288,9 +347,9 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
                 const Words<D> vin = buf[u];
                 buf[u] = load_next();
                 if (u & 1)
-                    step(std::integral_constant<int, 1>{}, vin, s + u);
+                    step(Par1{}, Steady{}, vin, s + u);
                 else
-                    step(std::integral_constant<int, 0>{}, vin, s + u);
+                    step(Par0{}, Steady{}, vin, s + u);
             }
         }
     } else {
@@ -298,16 +357,17 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
         // distance costs no registers and no register moves.  A row chunk is D DMAs of 64
         // consecutive words (lane L of DMA i fetches word base + 64i + L), read back as the
         // lane's D consecutive words.  Each step waits (by hand: the compiler does not track
-        // LDS-DMA completion) until its row's DMAs have landed: a step issues D DMAs and one
-        // store, so after the last DMA for step t this wave issued store(t-PL) and (D DMAs,
-        // store) for PL-1 steps, (D+1)(PL-1)+1 younger VMEM ops; the wait leaves a margin of 2.
+        // LDS-DMA completion) until its row's DMAs have landed: a step issues D DMAs and NSTORE
+        // stores, so after the last DMA for step t this wave issued NSTORE stores of step t and
+        // (D + NSTORE) ops for each of the PL-1 steps after it; the wait leaves a margin of 2.
         constexpr int PL = 8;
-        constexpr int kWait = (D + 1) * (PL - 1) - 1;
+        constexpr int kWait = NSTORE + (D + NSTORE) * (PL - 1) - 2;
+        static_assert(kWait <= 63, "vmcnt field");
         __shared__ __attribute__((aligned(16))) uint32_t ring[4][PL][64 * D];
         const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
         int dcol[D];
         {
-            const int base = ((int)chunk * 62 - 1) * D;
+            const int base = (int)chunk * stride - D;
 #pragma unroll
             for (int i = 0; i < D; ++i) dcol[i] = (base + 64 * i + lane + p.wd) % p.wd;
         }
@@ -329,24 +389,36 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
 #pragma unroll
         for (int u = 0; u < PL; ++u) {
             dma_next(u);
-            // dummy (dropped) store keeps the (DMA, store) cadence; distinct offsets so no
+            // dummy (dropped) stores keep the (DMA, stores) cadence; distinct offsets so no
             // dead-store elimination merges them
-            buffer_store_words<D>(orsrc, kOutOfRange + 8 * u, zero);
+            store_row(zero, kOutOfRange + 8 * u);
             asm volatile("" ::: "memory");
         }
-        for (int s = 0; s < nsteps; s += PL) {
+        auto one_step = [&](int u, auto fill, int st) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kWait) : "memory");
+            Words<D> vin;
 #pragma unroll
-            for (int u = 0; u < PL; ++u) {
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kWait) : "memory");
-                Words<D> vin;
+            for (int d = 0; d < D; ++d) vin.w[d] = ring[w][u][lane * D + d];
+            dma_next(u);
+            if (st & 1)
+                step(Par1{}, fill, vin, st);
+            else
+                step(Par0{}, fill, vin, st);
+        };
+        int s = 0;
+        // Pipeline fill of the chained levels (2K steps, fully unrolled so every level's
+        // skip / ingest-only / full decision is a compile-time constant: no branches, no extra
+        // registers).  Needs 2K to be a multiple of the ring depth so the main loop stays aligned.
+        if constexpr (!SKEW && (2 * K) % PL == 0) {
+            static_for(std::make_integer_sequence<int, 2 * K>{}, [&](auto stc) {
+                constexpr int ST = decltype(stc)::value;
+                one_step(ST % PL, stc, ST);
+            });
+            s = 2 * K;
+        }
+        for (; s < nsteps; s += PL) {
 #pragma unroll
-                for (int d = 0; d < D; ++d) vin.w[d] = ring[w][u][lane * D + d];
-                dma_next(u);
-                if (u & 1)
-                    step(std::integral_constant<int, 1>{}, vin, s + u);
-                else
-                    step(std::integral_constant<int, 0>{}, vin, s + u);
-            }
+            for (int u = 0; u < PL; ++u) one_step(u, Steady{}, s + u);
         }
         // Drain the ring's in-flight DMAs before the wave can retire: a DMA landing after the
         // workgroup released its LDS would write into the next workgroup's ring.
@@ -356,7 +428,7 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
     if (COUNT) {
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            uint32_t v = owned ? acc[j] : 0u;
+            uint32_t v = acc[j];
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
             if (lane == 0 && v)
@@ -622,6 +694,9 @@ inline size_t lds_pad_bytes() {
     return pad;
 }
 
+template <int K, int D>
+constexpr bool kHalfHalo = D == 1 && K <= 16;  // keep in sync with chunk_words()
+
 template <int K, bool SKEW, int D, int PF = 0>
 hipError_t launch_stencil_k(const uint32_t *in, uint32_t *out, const StencilParams &p,
                             unsigned long long *slots, hipStream_t s) {
@@ -629,10 +704,10 @@ hipError_t launch_stencil_k(const uint32_t *in, uint32_t *out, const StencilPara
     const unsigned blocks = (unsigned)((waves + 3) / 4);
     if (blocks == 0) return hipSuccess;
     if (slots)
-        hipLaunchKernelGGL((gol_stencil<K, true, SKEW, D, PF>), dim3(blocks), dim3(256),
+        hipLaunchKernelGGL((gol_stencil<K, true, SKEW, D, PF, kHalfHalo<K, D>>), dim3(blocks), dim3(256),
                            lds_pad_bytes(), s, in, out, p, slots);
     else
-        hipLaunchKernelGGL((gol_stencil<K, false, SKEW, D, PF>), dim3(blocks), dim3(256),
+        hipLaunchKernelGGL((gol_stencil<K, false, SKEW, D, PF, kHalfHalo<K, D>>), dim3(blocks), dim3(256),
                            lds_pad_bytes(), s, in, out, p, slots);
     return hipGetLastError();
 }
@@ -655,14 +730,14 @@ hipError_t launch_variant(int variant, const uint32_t *in, uint32_t *out, const 
 template <int K>
 const void *variant_fn(int variant) {
     switch (variant) {
-        case kVariantChain: return (const void *)gol_stencil<K, false, false, 1, 0>;
-        case kVariantSkewD2: return (const void *)gol_stencil<K, false, true, 2, 0>;
-        case kVariantChainD2: return (const void *)gol_stencil<K, false, false, 2, 0>;
-        case kVariantSkewLdsPf: return (const void *)gol_stencil<K, false, true, 1, 1>;
-        case kVariantChainLdsPf: return (const void *)gol_stencil<K, false, false, 1, 1>;
-        case kVariantSkewLdsD2: return (const void *)gol_stencil<K, false, true, 2, 1>;
-        case kVariantChainLdsD2: return (const void *)gol_stencil<K, false, false, 2, 1>;
-        default: return (const void *)gol_stencil<K, false, true, 1, 0>;
+        case kVariantChain: return (const void *)gol_stencil<K, false, false, 1, 0, kHalfHalo<K, 1>>;
+        case kVariantSkewD2: return (const void *)gol_stencil<K, false, true, 2, 0, kHalfHalo<K, 2>>;
+        case kVariantChainD2: return (const void *)gol_stencil<K, false, false, 2, 0, kHalfHalo<K, 2>>;
+        case kVariantSkewLdsPf: return (const void *)gol_stencil<K, false, true, 1, 1, kHalfHalo<K, 1>>;
+        case kVariantChainLdsPf: return (const void *)gol_stencil<K, false, false, 1, 1, kHalfHalo<K, 1>>;
+        case kVariantSkewLdsD2: return (const void *)gol_stencil<K, false, true, 2, 1, kHalfHalo<K, 2>>;
+        case kVariantChainLdsD2: return (const void *)gol_stencil<K, false, false, 2, 1, kHalfHalo<K, 2>>;
+        default: return (const void *)gol_stencil<K, false, true, 1, 0, kHalfHalo<K, 1>>;
     }
 }
 
