@@ -36,7 +36,8 @@ struct Shard {
     int rank = 0;
     int64_t y0 = 0, rows = 0;
     hipStream_t compute = nullptr, comm = nullptr;
-    hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
+    hipStream_t edge = nullptr;  // boundary bands of a split board, concurrent with the interior
+    hipEvent_t ev_ready = nullptr, ev_halo = nullptr, ev_edge = nullptr;
     uint32_t *buf[2] = {nullptr, nullptr};  // allocation base (halo rows first)
     unsigned long long *slots = nullptr;    // kMaxK * kCountSlots
     unsigned long long *scratch_u64 = nullptr;
@@ -146,8 +147,10 @@ int alloc_shard(golhip_t h, Shard &s) {
     HIPCHK(h, hipSetDevice(s.device));
     HIPCHK(h, hipStreamCreateWithFlags(&s.compute, hipStreamNonBlocking));
     HIPCHK(h, hipStreamCreateWithFlags(&s.comm, hipStreamNonBlocking));
+    HIPCHK(h, hipStreamCreateWithFlags(&s.edge, hipStreamNonBlocking));
     HIPCHK(h, hipEventCreateWithFlags(&s.ev_ready, hipEventDisableTiming));
     HIPCHK(h, hipEventCreateWithFlags(&s.ev_halo, hipEventDisableTiming));
+    HIPCHK(h, hipEventCreateWithFlags(&s.ev_edge, hipEventDisableTiming));
     const size_t words = (size_t)(s.rows + 2 * (int64_t)h->halo) * (size_t)h->pitch;
     for (int i = 0; i < 2; ++i) {
         HIPCHK(h, hipMalloc(&s.buf[i], words * sizeof(uint32_t)));
@@ -166,6 +169,7 @@ void free_shard(Shard &s) {
     (void)hipSetDevice(s.device);
     if (s.compute) (void)hipStreamSynchronize(s.compute);
     if (s.comm) (void)hipStreamSynchronize(s.comm);
+    if (s.edge) (void)hipStreamSynchronize(s.edge);
     if (s.comm_nccl) (void)ncclCommDestroy(s.comm_nccl);
     for (auto &b : s.buf)
         if (b) (void)hipFree(b);
@@ -174,8 +178,10 @@ void free_shard(Shard &s) {
     if (s.d_counts) (void)hipFree(s.d_counts);
     if (s.ev_ready) (void)hipEventDestroy(s.ev_ready);
     if (s.ev_halo) (void)hipEventDestroy(s.ev_halo);
+    if (s.ev_edge) (void)hipEventDestroy(s.ev_edge);
     if (s.compute) (void)hipStreamDestroy(s.compute);
     if (s.comm) (void)hipStreamDestroy(s.comm);
+    if (s.edge) (void)hipStreamDestroy(s.edge);
     s = Shard{};
 }
 
@@ -261,7 +267,7 @@ int64_t auto_band(golhip_t h, int64_t rows_total, int K, int64_t reserve_waves =
 }
 
 StencilParams make_params(golhip_t h, const Shard &s, int K, int64_t r0b, int64_t r0e,
-                          int64_t r1b, int64_t r1e) {
+                          int64_t r1b, int64_t r1e, int64_t reserve_waves = 0) {
     StencilParams p{};
     p.pitch = h->pitch;
     p.r0b = r0b;
@@ -269,7 +275,7 @@ StencilParams make_params(golhip_t h, const Shard &s, int K, int64_t r0b, int64_
     p.r1b = r1b;
     p.r1e = r1e;
     const int64_t total = (r0e - r0b) + (r1e - r1b);
-    p.band = auto_band(h, std::max<int64_t>(total, 1), K);
+    p.band = auto_band(h, std::max<int64_t>(total, 1), K, reserve_waves);
     p.nbands0 = (r0e - r0b + p.band - 1) / p.band;
     p.nbands = p.nbands0 + (r1e - r1b + p.band - 1) / p.band;
     p.wrap_rows = h->split ? 0 : h->height;
@@ -385,12 +391,18 @@ int step_block(golhip_t h, int K, int64_t counts_off) {
             StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0);
             HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, p, slots, s.compute));
         } else if (s.rows >= 3 * K) {
-            // interior rows need no halo: overlap them with the exchange
-            StencilParams pi = make_params(h, s, K, K, s.rows - K, 0, 0);
-            HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, pi, slots, s.compute));
-            HIPCHK(h, hipStreamWaitEvent(s.compute, s.ev_halo, 0));
+            // The interior rows need no halo: they run while the halos are exchanged.  The two
+            // boundary bands wait for the halos on their own stream and run concurrently with the
+            // interior, in wave slots the interior launch leaves free for them; the compute stream
+            // then joins them (counts and the next block need both).
             StencilParams pb = make_params(h, s, K, 0, K, s.rows - K, s.rows);
-            HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, pb, slots, s.compute));
+            const int64_t edge_waves = pb.nbands * (int64_t)pb.nchunks;
+            StencilParams pi = make_params(h, s, K, K, s.rows - K, 0, 0, edge_waves);
+            HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, pi, slots, s.compute));
+            HIPCHK(h, hipStreamWaitEvent(s.edge, s.ev_halo, 0));
+            HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, pb, slots, s.edge));
+            HIPCHK(h, hipEventRecord(s.ev_edge, s.edge));
+            HIPCHK(h, hipStreamWaitEvent(s.compute, s.ev_edge, 0));
         } else {
             HIPCHK(h, hipStreamWaitEvent(s.compute, s.ev_halo, 0));
             StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0);
@@ -414,6 +426,7 @@ int sync_all(golhip_t h) {
     for (auto &s : h->shards) {
         HIPCHK(h, hipSetDevice(s.device));
         HIPCHK(h, hipStreamSynchronize(s.comm));
+        HIPCHK(h, hipStreamSynchronize(s.edge));
         HIPCHK(h, hipStreamSynchronize(s.compute));
     }
     return GOLHIP_OK;
