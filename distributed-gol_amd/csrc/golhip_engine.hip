@@ -235,8 +235,7 @@ int64_t auto_band(golhip_t h, int64_t rows_total, int K, int64_t reserve_waves =
     const int64_t per = golhip::chunk_words(K, h->variant);
     const int64_t nchunks = (h->wd + per - 1) / per;
     // Fill the chip in whole rounds of resident waves (CUs x resident waves per CU), so every
-    // SIMD gets the same number of equal bands; a band is at least 2K rows (the pipeline fill of
-    // a K-level band is 2K..3K steps).
+    // SIMD gets the same number of equal bands.
     if (h->cus == 0) {
         hipDeviceProp_t prop;
         h->cus = hipGetDeviceProperties(&prop, h->shards[0].device) == hipSuccess
@@ -254,7 +253,10 @@ int64_t auto_band(golhip_t h, int64_t rows_total, int K, int64_t reserve_waves =
     const int64_t slots = std::max<int64_t>(1, (capacity - reserve_waves) / nchunks);
     const int64_t rounds = (rows_total + slots * kMaxBand - 1) / (slots * kMaxBand);
     int64_t band = (rows_total + rounds * slots - 1) / (rounds * slots);
-    band = std::max<int64_t>(band, std::min<int64_t>(2 * K, rows_total));
+    // Small boards (fewer rows than a round of minimal bands) are latency-bound: a wave's work is
+    // band*K level updates plus the K(K-1) of its pipeline fill, so bands shorter than K mostly
+    // add fill; K-row bands measured best (profiles/r01_tune_small_*).
+    band = std::max<int64_t>(band, std::min<int64_t>(std::max(K, 8), rows_total));
     band = std::max<int64_t>(band, 1);
     // A wave runs band + lag steps in blocks of 8 (the kernel's prefetch ring); round the band so
     // that full bands end on a block boundary instead of computing up to 7 discarded rows.

@@ -24,7 +24,7 @@ struct StencilParams {
     int64_t wrap_rows;   // > 0: single strip holding the whole torus height (row index mod H)
     int64_t lo, hi;      // halo mode: readable input rows [lo, hi) relative to row 0
     int32_t wd;          // words per row of the torus
-    int32_t nchunks;     // column chunks per row: lanes 1..62 own D words each, 0 and 63 are halo
+    int32_t nchunks;     // column chunks per row (chunk_words() words each)
 };
 
 constexpr int kMaxK = 32;         // generations per launch limit (halo lane = 32 bits)

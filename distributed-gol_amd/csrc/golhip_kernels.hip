@@ -432,21 +432,23 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
             if (lane == 0 && v)
-                atomicAdd(&slots[j * kCountSlots + (int)(wave & (kCountSlots - 1))],
-                          (unsigned long long)v);
+                __hip_atomic_fetch_add(&slots[j * kCountSlots + (int)(wave & (kCountSlots - 1))],
+                                       (unsigned long long)v, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
 
-__global__ void count_finalize(int K, unsigned long long *slots, unsigned long long *counts) {
-    const int j = threadIdx.x;
-    if (j >= K) return;
-    unsigned long long s = 0;
-    for (int i = 0; i < kCountSlots; ++i) {
-        s += slots[j * kCountSlots + i];
-        slots[j * kCountSlots + i] = 0;
-    }
-    counts[j] = s;
+// Per-generation counts of a launch whose slots were not finalized in-kernel: block j sums
+// generation j's kCountSlots slots (one per lane) and re-zeroes them.
+__global__ void count_finalize(unsigned long long *slots, unsigned long long *counts) {
+    const int j = blockIdx.x, lane = threadIdx.x;
+    unsigned long long *sl = &slots[j * kCountSlots + lane];
+    unsigned long long x = *sl;
+    *sl = 0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    if (lane == 0) counts[j] = x;
 }
 
 // ------------------------------------------------------------------ board I/O (gol/io.go)
@@ -783,7 +785,8 @@ int stencil_waves_per_cu(int K, int variant) {
 
 hipError_t launch_count_finalize(int K, unsigned long long *slots, unsigned long long *counts,
                                  hipStream_t s) {
-    hipLaunchKernelGGL(count_finalize, dim3(1), dim3(64), 0, s, K, slots, counts);
+    static_assert(kCountSlots == 64, "one slot per lane");
+    hipLaunchKernelGGL(count_finalize, dim3(K), dim3(64), 0, s, slots, counts);
     return hipGetLastError();
 }
 
