@@ -7,11 +7,12 @@
 // it as a per-generation popcount.
 //
 // Mapping (see DESIGN.md for the roofline):
-//   * one lane = one 32-bit word (32 cells) of a row; a wave = 64 consecutive words of a row:
-//     lanes 1..62 own their word, lanes 0 and 63 are horizontal halo (their outer bits go stale
-//     one bit per generation, so K <= 32 keeps every owned bit exact);
+//   * one lane = one 32-bit word (32 cells) of a row; a wave = 64 consecutive words of a row.
+//     The outer bits of lanes 0 and 63 go stale one bit per generation (their outer neighbour
+//     is outside the wave): for K <= 16 lane 0 still owns its upper and lane 63 its lower half
+//     word (63 words per wave), for K <= 32 lanes 0 and 63 are pure halo (62 words per wave);
 //   * horizontal neighbours cross lanes with DPP wave_shr:1 / wave_shl:1 and are merged with
-//     v_alignbit; the 9-cell sums use v_bitop3 (gfx950) full adders;
+//     v_alignbit; the sums and the rule are v_bitop3 (gfx950): 13 VALU per word per generation;
 //   * each wave streams down a band of rows keeping, per generation level, the last two rows'
 //     (sum, carry, cell) in registers: one input row in -> one row out per level per step, so a
 //     launch advances K generations while reading the board once and writing it once.
@@ -110,14 +111,6 @@ __device__ __forceinline__ void level_update(RowState<D> &above, const RowState<
 }
 
 template <int D>
-__device__ __forceinline__ uint32_t popc_words(const Words<D> &x) {
-    uint32_t c = 0;
-#pragma unroll
-    for (int d = 0; d < D; ++d) c += __builtin_popcount(x.w[d]);
-    return c;
-}
-
-template <int D>
 __device__ __forceinline__ Words<D> load_words(const uint32_t *p) {
     Words<D> v;
     if constexpr (D == 2) {
@@ -146,24 +139,6 @@ __device__ __forceinline__ void buffer_store_words(__amdgpu_buffer_rsrc_t r, int
     } else {
         __builtin_amdgcn_raw_buffer_store_b32((int)v.w[0], r, off, 0, 0);
     }
-}
-
-// A copy the register allocator cannot coalesce away: moving a consumed ring slot into a fresh
-// register lets the refill load of that slot target the same register every iteration.
-template <int D>
-__device__ __forceinline__ Words<D> opaque_copy(const Words<D> &v) {
-    Words<D> r;
-#pragma unroll
-    for (int d = 0; d < D; ++d) asm volatile("v_mov_b32 %0, %1" : "=v"(r.w[d]) : "v"(v.w[d]));
-    return r;
-}
-
-template <int D>
-__device__ __forceinline__ void store_words(uint32_t *p, const Words<D> &v) {
-    if constexpr (D == 2)
-        *reinterpret_cast<uint2 *>(p) = make_uint2(v.w[0], v.w[1]);
-    else
-        *p = v.w[0];
 }
 
 template <int... I, class F>

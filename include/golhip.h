@@ -94,7 +94,10 @@ int golhip_create(int width, int height, int ngpus, int k, golhip_t *out);
  * nstrips > ndevices exercises the multi-strip path on fewer GPUs. */
 int golhip_create_strips(int width, int height, int nstrips, int ndevices, int k, golhip_t *out);
 /* One process per GPU: rank `rank` of `world_size`, on HIP device `device`. nccl_id: the
- * GOLHIP_NCCL_ID_BYTES produced by golhip_nccl_unique_id() on rank 0 (NULL if world_size == 1). */
+ * GOLHIP_NCCL_ID_BYTES produced by golhip_nccl_unique_id() on rank 0 (NULL if world_size == 1).
+ * Test hook: with world_size == 1 and the environment variable GOLHIP_RING_SELF=1 the board is a
+ * ring of ONE halo'd strip whose halos go through RCCL send/recv to itself (the rank-mode path
+ * on a single GPU). */
 int golhip_nccl_unique_id(uint8_t *out /* GOLHIP_NCCL_ID_BYTES */);
 int golhip_create_rank(int width, int height, int rank, int world_size, int device, int k,
                        const uint8_t *nccl_id, golhip_t *out);
