@@ -13,6 +13,8 @@ other boards (e.g. --size 262144 for configs[3], strong scaling).
 Prints ONE JSON line on rank 0 (keys per the driver contract), plus:
   roofline     : algorithmic bytes (0.25 B per cell-update) per stencil launch / the launch's
                  average duration from HIP events recorded on the engine's compute stream;
+  valu_roofline: the stencil's actual bound for k >= 4 -- algorithmic wave64 VALU instructions
+                 (13 per 32-cell word per generation) per second vs the issue peak of that mix;
   cpu_baseline : the reference algorithm (oracle/ port of server/server.go + broker split,
                  byte per cell, 4 servers x T threads) timed on this host on a bounded sample;
   k_sweep      : GCUPS per temporal-blocking depth k (N == 1 only).
@@ -36,6 +38,14 @@ import golhip  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 BYTES_PER_CELL_UPDATE = 0.25  # 1 packed bit read + 1 packed bit written per cell per generation
+# VALU roofline of the stencil (the bound for k >= 4): 13 wave64 VALU
+# instructions per 32-cell word per generation (9 v_bitop3 at full rate, 2 v_alignbit + 2 DPP
+# moves at half rate).  Peak issue = 1024 SIMDs x 2.4 GHz / cycles per instruction, where a
+# full-rate wave64 op takes 2 cycles (SIMD-32) and a half-rate one 4: the mix averages 34 cycles
+# per 13 instructions.  Reported as instruction issue rate (wave64 VALU instructions per second).
+VALU_PER_WORD_GEN = 13
+VALU_CYCLES_PER_WORD_GEN = 9 * 2 + 4 * 4
+SIMDS, PEAK_CLOCK_GHZ = 1024, 2.4
 
 
 def parse():
@@ -153,6 +163,16 @@ def main():
     gens_per_launch = gens / max(launches, 1)
     alg_bytes_per_launch = BYTES_PER_CELL_UPDATE * local_cells * gens_per_launch
     achieved = alg_bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
+    # VALU roofline: algorithmic wave-instructions per launch (the cells it updates, no halo or
+    # pipeline-fill work) over the launch time, against the issue peak for the same mix
+    words_per_launch = local_cells / 32 * gens_per_launch
+    valu_instr = words_per_launch / 64 * VALU_PER_WORD_GEN
+    valu_achieved = valu_instr / (avg_launch_ms * 1e-3) / 1e12
+    valu_peak = SIMDS * PEAK_CLOCK_GHZ * 1e9 / (VALU_CYCLES_PER_WORD_GEN / VALU_PER_WORD_GEN) / 1e12
+    valu = {"bound": "valu", "achieved": round(valu_achieved, 4), "peak": round(valu_peak, 4),
+            "unit": "T wave64-instr/s", "frac": round(valu_achieved / valu_peak, 4),
+            "mix": "13 per 32-cell word per generation: 9 v_bitop3 (2 cyc) + 2 v_alignbit + 2 DPP (4 cyc)",
+            "note": "peak at 2.4 GHz; the dense start runs at 1.9-2.2 GHz (power)"}
     traffic = None
     try:
         pmc = json.loads(Path(a.pmc_file).read_text())
@@ -210,6 +230,7 @@ def main():
                 "avg_launch_us": round(avg_launch_ms * 1e3, 2),
                 "gens_per_launch": gens_per_launch,
             },
+            "valu_roofline": valu,
             "cpu_baseline": cpu,
             "k_sweep_gcups": sweep,
             "alive_after_timed": int(alive_timed),
