@@ -72,6 +72,7 @@ struct golhip_engine {
     int waves_per_cu[golhip::kMaxK + 1][golhip::kNumVariants] = {};  // occupancy cache per (K, variant)
     bool rank_mode = false;
     bool split = false;  // board held as halo'd row strips (world > 1, or GOLHIP_RING_SELF)
+    int force_split = 0;  // GOLHIP_SPLIT (0 = automatic)
     std::vector<Shard> shards;
     int cur = 0;
     bool prev_valid = false;
@@ -205,6 +206,7 @@ int setup_engine(golhip_t h, int width, int height, int world, int k) {
     h->split = world > 1;
     h->halo = h->split ? k : 0;
     if (const char *e = std::getenv("GOLHIP_BAND_ROWS")) h->band_rows = std::atoi(e);
+    if (const char *e = std::getenv("GOLHIP_SPLIT")) h->force_split = std::atoi(e);
     if (const char *e = std::getenv("GOLHIP_VARIANT"))
         h->variant = std::strcmp(e, "chain") == 0     ? golhip::kVariantChain
                      : std::strcmp(e, "skew") == 0   ? golhip::kVariantSkew
@@ -266,6 +268,38 @@ int64_t auto_band(golhip_t h, int64_t rows_total, int K, int64_t reserve_waves =
     const int64_t lag = skew ? 3 * K - 1 : 2 * K;
     if (band < rows_total) band = std::max<int64_t>(8, (band + lag + 7) / 8 * 8 - lag);
     return band;
+}
+
+// Waves per (band, chunk) of a launch over rows_total rows: the level-split kernel (S = 2 or 4)
+// when even minimal bands leave the chip short of waves (small boards, latency-bound), else 1.
+// GOLHIP_SPLIT=1/2/4 forces it (tests, tuning).
+int pick_split(golhip_t h, int64_t rows_total, int K) {
+    if (h->variant != golhip::kVariantChainLdsPf) return 1;
+    if (h->force_split > 0)
+        return h->force_split > 1 && golhip::stencil_split_supported(K, h->force_split)
+                   ? h->force_split
+                   : 1;
+    // measured (profiles/r01_tune_small.txt): a gain at K = 16 (-10 % per turn at 5120^2), none
+    // at K = 12 and a loss at K = 8, where the lockstep barriers cost more than the shorter chain
+    if (K < 16) return 1;
+    const int64_t per = golhip::chunk_words(K, h->variant);
+    const int64_t nchunks = (h->wd + per - 1) / per;
+    const int64_t minband = std::max(K, 8);
+    const int64_t waves1 = (rows_total + minband - 1) / minband * nchunks;
+    int &wpc = h->waves_per_cu[K][h->variant];
+    if (wpc == 0) wpc = golhip::stencil_waves_per_cu(K, h->variant);
+    const int64_t capacity = (int64_t)h->cus * wpc;
+    for (int S : {4, 2})
+        if (golhip::stencil_split_supported(K, S) && waves1 * S <= capacity) return S;
+    return 1;
+}
+
+// Launch the K-generation stencil described by p (level-split kernel when pick_split says so).
+hipError_t launch_auto(golhip_t h, int K, const uint32_t *in, uint32_t *out,
+                       const StencilParams &p, unsigned long long *slots, hipStream_t s) {
+    const int S = pick_split(h, (p.r0e - p.r0b) + (p.r1e - p.r1b), K);
+    if (S > 1) return golhip::launch_stencil_split(K, S, in, out, p, slots, s);
+    return golhip::launch_stencil(K, h->variant, in, out, p, slots, s);
 }
 
 StencilParams make_params(golhip_t h, const Shard &s, int K, int64_t r0b, int64_t r0e,
@@ -391,7 +425,7 @@ int step_block(golhip_t h, int K, int64_t counts_off) {
         uint32_t *out = h->row0(s, nxt);
         if (!h->split) {
             StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0);
-            HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, p, slots, s.compute));
+            HIPCHK(h, launch_auto(h, K, in, out, p, slots, s.compute));
         } else if (s.rows >= 3 * K) {
             // The interior rows need no halo: they run while the halos are exchanged.  The two
             // boundary bands wait for the halos on their own stream and run concurrently with the
@@ -590,8 +624,8 @@ int graph_for(golhip_t h, int K, int M, bool counting, hipGraphExec_t *out) {
     for (int i = 0; i < M && err == hipSuccess; ++i) {
         const int c = h->cur ^ (i & 1);
         StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0);
-        err = golhip::launch_stencil(K, h->variant, h->row0(s, c), h->row0(s, c ^ 1), p,
-                                     counting ? s.slots : nullptr, s.compute);
+        err = launch_auto(h, K, h->row0(s, c), h->row0(s, c ^ 1), p,
+                          counting ? s.slots : nullptr, s.compute);
         if (err == hipSuccess && counting)
             err = golhip::launch_count_finalize(K, s.slots, h->g_counts + (int64_t)i * K,
                                                 s.compute);

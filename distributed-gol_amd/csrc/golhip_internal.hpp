@@ -60,6 +60,12 @@ hipError_t launch_stencil(int K, int variant, const uint32_t *in_row0, uint32_t 
                           const StencilParams &p, unsigned long long *count_slots,
                           hipStream_t s);
 bool stencil_k_supported(int K);
+// Level-split stencil (small boards): the K levels of a (band, chunk) over a workgroup of S waves
+// (S = 2 or 4, D = 1, LDS-DMA input, chained levels; same geometry as kVariantChainLdsPf).
+hipError_t launch_stencil_split(int K, int S, const uint32_t *in_row0, uint32_t *out_row0,
+                                const StencilParams &p, unsigned long long *count_slots,
+                                hipStream_t s);
+bool stencil_split_supported(int K, int S);
 // Resident waves per CU of the stencil launch (occupancy query), for sizing the grid.
 int stencil_waves_per_cu(int K, int variant);
 // Sum the slots of K generations into counts[0..K) and zero the slots.

@@ -154,6 +154,97 @@ __device__ __forceinline__ void level_ingest(RowState<D> &above, const Words<D> 
     above.c = in;
 }
 
+// Output rows [ya, yb) of band `bandi` of a launch (range 0 bands first, then range 1).
+// Row indices fit in 32 bits; keeping every loop-carried counter 32-bit keeps the compares on the
+// SALU (gfx9 has no 64-bit signed s_cmp, a 64-bit compare would drag them into VGPRs).
+__device__ __forceinline__ void band_rows(const StencilParams &p, int64_t bandi, int &ya, int &yb) {
+    if (bandi < p.nbands0) {
+        ya = (int)(p.r0b + bandi * p.band);
+        yb = (int)min((int64_t)ya + p.band, p.r0e);
+    } else {
+        ya = (int)(p.r1b + (bandi - p.nbands0) * p.band);
+        yb = (int)min((int64_t)ya + p.band, p.r1e);
+    }
+}
+
+// Input row stream of a band: rows ya-K, ya-K+1, ... wrapped mod H (single strip holding the
+// torus) or clamped to the halo'd strip [lo, hi).  Branch-free (scalar selects), so the waitcnt
+// pass sees one straight line of loads and stores and keeps the full prefetch distance.
+struct RowStream {
+    int ly, wrap, hi;
+    __device__ __forceinline__ RowStream(const StencilParams &p, int first) {
+        wrap = (int)p.wrap_rows;
+        hi = (int)p.hi;
+        const int lo = (int)p.lo;
+        ly = first;
+        if (wrap > 0) {
+            ly %= wrap;
+            if (ly < 0) ly += wrap;
+        } else {
+            ly = ly < lo ? lo : (ly >= hi ? hi - 1 : ly);
+        }
+    }
+    __device__ __forceinline__ void advance() {
+        const int nx = ly + 1;
+        ly = wrap > 0 ? (nx == wrap ? 0 : nx) : (nx < hi ? nx : hi - 1);
+    }
+};
+
+// Where a lane stores its (first) word: through at most one of a full store (off_full), the low
+// half (off_lo) or the high half (off_hi, HH only); the others point past the buffer descriptor
+// and are dropped.  own_mask: the owned cells of the word, for the counts.
+struct LaneStore {
+    int off_full = kOutOfRange, off_lo = kOutOfRange, off_hi = kOutOfRange;
+    uint32_t own_mask = 0;
+};
+template <bool HH>
+__device__ __forceinline__ LaneStore lane_store(int lane, int colraw, int col, int wd) {
+    LaneStore o;
+    if (HH) {
+        // owned unwrapped cells: [-16, 32wd - 16); lane 0 -> upper half, lane 63 -> lower half
+        const int last = wd - 1;
+        if (lane == 0) {
+            if (colraw <= last - 1) { o.off_hi = col * 4 + 2; o.own_mask = 0xffff0000u; }
+        } else if (lane == 63) {
+            if (colraw <= last) { o.off_lo = col * 4; o.own_mask = 0x0000ffffu; }
+        } else if (colraw < last) {
+            o.off_full = col * 4; o.own_mask = ~0u;
+        } else if (colraw == last) {
+            o.off_lo = col * 4; o.own_mask = 0x0000ffffu;
+        }
+    } else if (lane >= 1 && lane <= 62 && colraw < wd) {
+        o.off_full = col * 4;
+        o.own_mask = ~0u;
+    }
+    return o;
+}
+
+template <int D, bool HH>
+__device__ __forceinline__ void store_row(__amdgpu_buffer_rsrc_t r, const LaneStore &ls,
+                                          const Words<D> &v, int rowoff) {
+    buffer_store_words<D>(r, ls.off_full + rowoff, v);
+    if (HH) {
+        __builtin_amdgcn_raw_buffer_store_b16((short)v.w[0], r, ls.off_lo + rowoff, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b16((short)(v.w[0] >> 16), r, ls.off_hi + rowoff, 0, 0);
+    }
+}
+
+// Per-level alive counts of a wave -> its spread slot of each generation (agent-scope atomics).
+template <int NL>
+__device__ __forceinline__ void flush_counts(const uint32_t (&acc)[NL], int j0, int lane,
+                                             int64_t wave, unsigned long long *slots) {
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+        uint32_t v = acc[j];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        if (lane == 0 && v)
+            __hip_atomic_fetch_add(&slots[(j0 + j) * kCountSlots + (int)(wave & (kCountSlots - 1))],
+                                   (unsigned long long)v, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // Column geometry of a wave's 64 lanes (shared with the host via chunk_words()):
 //   default : lanes 1..62 own D words each, lanes 0 and 63 are the horizontal halo (K <= 32);
 //   HH      : (D = 1, K <= 16) a halo needs only K <= 16 bits, so lane 0 owns the upper and lane 63
@@ -176,72 +267,26 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
     const int64_t chunk = wave % p.nchunks;
     const int64_t bandi = wave / p.nchunks;
     if (bandi >= p.nbands) return;  // wave-uniform
-    // Row indices fit in 32 bits; keeping every loop-carried counter 32-bit keeps the compares
-    // on the SALU (gfx9 has no 64-bit signed s_cmp, a 64-bit compare would drag them into VGPRs).
     int ya, yb;
-    if (bandi < p.nbands0) {
-        ya = (int)(p.r0b + bandi * p.band);
-        yb = (int)min((int64_t)ya + p.band, p.r0e);
-    } else {
-        ya = (int)(p.r1b + (bandi - p.nbands0) * p.band);
-        yb = (int)min((int64_t)ya + p.band, p.r1e);
-    }
+    band_rows(p, bandi, ya, yb);
     // First word (unwrapped) of this lane and its wrapped column.
     const int stride = HH ? 63 : 62 * D;
     const int colraw = (int)chunk * stride + (lane - 1) * D;
     const int col = (colraw + p.wd) % p.wd;
-
-    // Input row stream: rows ya-K, ya-K+1, ... (wrap mod H, or clamped to the halo'd strip).
-    // Row pointers are wave-uniform (SGPRs); the lane adds its column.
-    const int wrap = (int)p.wrap_rows, lo = (int)p.lo, hi = (int)p.hi;
-    int ly = ya - K;
-    if (wrap > 0) {
-        ly %= wrap;
-        if (ly < 0) ly += wrap;
-    } else {
-        ly = ly < lo ? lo : (ly >= hi ? hi - 1 : ly);
-    }
-    // Next-row arithmetic is branch-free (scalar selects), so the waitcnt pass sees one straight
-    // line of loads and stores and keeps the full prefetch distance.
+    RowStream rows(p, ya - K);
     auto load_next = [&]() -> Words<D> {
-        const Words<D> v = load_words<D>(in + (int64_t)ly * p.pitch + col);
-        const int nx = ly + 1;
-        ly = wrap > 0 ? (nx == wrap ? 0 : nx) : (nx < hi ? nx : hi - 1);
+        const Words<D> v = load_words<D>(in + (int64_t)rows.ly * p.pitch + col);
+        rows.advance();
         return v;
     };
     // Output: one raw-buffer descriptor over the band's rows (offsets stay 32-bit for any board).
-    // Each lane stores through at most one of: a full store (off_full), the low half (off_lo) or
-    // the high half (off_hi, HH only); the others point past the descriptor and are dropped.
     const int rowbytes = (int)(p.pitch * 4);
     const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
         out + (int64_t)ya * p.pitch, 0, (yb - ya) * rowbytes, kBufferRsrcWord3);
-    int off_full = kOutOfRange, off_lo = kOutOfRange, off_hi = kOutOfRange;
-    uint32_t own_mask = 0;  // owned cells of the lane's (first) word, for the counts
-    if (HH) {
-        // owned unwrapped cells: [-16, 32wd - 16); lane 0 -> upper half, lane 63 -> lower half
-        const int last = p.wd - 1;
-        if (lane == 0) {
-            if (colraw <= last - 1) { off_hi = col * 4 + 2; own_mask = 0xffff0000u; }
-        } else if (lane == 63) {
-            if (colraw <= last) { off_lo = col * 4; own_mask = 0x0000ffffu; }
-        } else if (colraw < last) {
-            off_full = col * 4; own_mask = ~0u;
-        } else if (colraw == last) {
-            off_lo = col * 4; own_mask = 0x0000ffffu;
-        }
-    } else if (lane >= 1 && lane <= 62 && colraw < p.wd) {
-        off_full = col * 4;
-        own_mask = ~0u;
-    }
+    const LaneStore ls = lane_store<HH>(lane, colraw, col, p.wd);
+    const uint32_t own_mask = ls.own_mask;
     constexpr int NSTORE = HH ? 3 : 1;  // vector-memory stores per step
-    auto store_row = [&](const Words<D> &v, int rowoff) {
-        buffer_store_words<D>(orsrc, off_full + rowoff, v);
-        if (HH) {
-            __builtin_amdgcn_raw_buffer_store_b16((short)v.w[0], orsrc, off_lo + rowoff, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b16((short)(v.w[0] >> 16), orsrc, off_hi + rowoff, 0,
-                                                  0);
-        }
-    };
+    auto store_row = [&](const Words<D> &v, int rowoff) { golhip::store_row<D, HH>(orsrc, ls, v, rowoff); };
 
     // Per level: a two-slot ring (X/Y swap roles every step) and, skewed, the pending input row.
     RowState<D> X[K], Y[K];
@@ -349,14 +394,13 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
         // Compiler-level fences (empty asm with a memory clobber) keep every DMA and store in
         // program order, so the per-step vmcnt accounting holds whatever the scheduler does.
         auto dma_next = [&](int slot) {
-            const uint32_t *row = in + (int64_t)ly * p.pitch;
+            const uint32_t *row = in + (int64_t)rows.ly * p.pitch;
 #pragma unroll
             for (int i = 0; i < D; ++i) {
                 __builtin_amdgcn_global_load_lds(row + dcol[i], &ring[w][slot][64 * i], 4, 0, 0);
                 asm volatile("" ::: "memory");
             }
-            const int nx = ly + 1;
-            ly = wrap > 0 ? (nx == wrap ? 0 : nx) : (nx < hi ? nx : hi - 1);
+            rows.advance();
         };
         Words<D> zero;
 #pragma unroll
@@ -400,18 +444,138 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
 
-    if (COUNT) {
+    if (COUNT) flush_counts<K>(acc, 0, lane, wave, slots);
+}
+
+// ---------------------------------------------------------------- level-split stencil
+// Small boards are latency-bound: a round of minimal bands gives fewer waves than SIMDs, and a
+// lone wave's time is its dependent chain -- band*K level updates (+ the fill), K levels deep
+// per step.  gol_stencil_split spreads the K levels of one (band, chunk) over a workgroup of S
+// waves: wave R computes levels [R*K/S, (R+1)*K/S) and hands its last level's output row to wave
+// R+1 through LDS; the group steps in lockstep (one s_barrier per step), so every wave's chain is
+// K/S levels and the board runs S times as many waves, with no extra (halo) work.
+// Wave R's level j outputs row ya - K + st - (j+1) - R at step st (one step of delay per hand-off),
+// valid from step 2j + 2 + R; the final row (j = K-1, R = S-1) lags by 2K + S - 1 steps.
+template <int K, bool COUNT, int S, int R>
+__device__ __forceinline__ void split_role(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+                                           const StencilParams &p,
+                                           unsigned long long *__restrict__ slots, int64_t group,
+                                           int lane, uint32_t (*xring)[2][64],
+                                           uint32_t (*ring)[64]) {
+    constexpr bool HH = K <= 16;
+    constexpr int NL = K / S, J0 = R * NL;  // this wave's levels: [J0, J0 + NL)
+    constexpr int PL = 8;                   // LDS-DMA ring depth (wave 0)
+    constexpr int LAG = 2 * K + S - 1;
+    constexpr int FILL = (LAG + PL - 1) / PL * PL;  // unrolled fill steps (ring-aligned)
+    const int64_t chunk = group % p.nchunks, bandi = group / p.nchunks;
+    int ya, yb;
+    band_rows(p, bandi, ya, yb);
+    const int colraw = (int)chunk * (HH ? 63 : 62) + lane - 1;
+    const int col = (colraw + p.wd) % p.wd;
+    const int nrows = yb - ya, nsteps = nrows + LAG;
+    const int rowbytes = (int)(p.pitch * 4);
+    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+        out + (int64_t)ya * p.pitch, 0, (yb - ya) * rowbytes, kBufferRsrcWord3);
+    const LaneStore ls = lane_store<HH>(lane, colraw, col, p.wd);
+    RowStream rows(p, ya - K);
+
+    RowState<1> X[NL], Y[NL];
+    uint32_t acc[NL];
 #pragma unroll
-        for (int j = 0; j < K; ++j) {
-            uint32_t v = acc[j];
+    for (int j = 0; j < NL; ++j) {
+        X[j].s.w[0] = X[j].cy.w[0] = X[j].c.w[0] = 0;
+        Y[j].s.w[0] = Y[j].cy.w[0] = Y[j].c.w[0] = 0;
+        acc[j] = 0;
+    }
+    auto dma_next = [&](int slot) {
+        __builtin_amdgcn_global_load_lds(in + (int64_t)rows.ly * p.pitch + col, &ring[slot][0], 4, 0, 0);
+        asm volatile("" ::: "memory");
+        rows.advance();
+    };
+    if (R == 0) {
 #pragma unroll
-            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-            if (lane == 0 && v)
-                __hip_atomic_fetch_add(&slots[j * kCountSlots + (int)(wave & (kCountSlots - 1))],
-                                       (unsigned long long)v, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
+        for (int u = 0; u < PL; ++u) dma_next(u);
+    }
+    // One lockstep step: take the input row (DMA ring or the previous wave's hand-off), run this
+    // wave's levels (compile-time fill guards when FST >= 0), hand off or store, barrier.
+    auto step = [&](auto par, auto fill, int u, int st) {
+        constexpr int PAR = decltype(par)::value;
+        constexpr int FST = decltype(fill)::value;
+        Words<1> nc;
+        if (R == 0) {
+            // PL-1 younger DMAs after this slot's; margin of 2
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PL - 1 - 2) : "memory");
+            nc.w[0] = ring[u][lane];
+            dma_next(u);
+        } else {
+            nc.w[0] = xring[R - 1][(st - 1) & 1][lane];
+        }
+#pragma unroll
+        for (int jl = 0; jl < NL; ++jl) {
+            const int j = J0 + jl;
+            if (FST >= 0 && FST < 2 * j + 2 + R) {  // folds away: FST and (unrolled) j constant
+                if (FST >= 2 * j + R) level_ingest<1>(PAR == 0 ? X[jl] : Y[jl], nc);
+                nc.w[0] = 0;
+                continue;
+            }
+            Words<1> nx;
+            if (PAR == 0)
+                level_update<1>(X[jl], Y[jl], nc, nx);
+            else
+                level_update<1>(Y[jl], X[jl], nc, nx);
+            if (COUNT) {
+                const int rr = st - K - (j + 1) - R;
+                if (rr >= 0 && rr < nrows) acc[jl] += __builtin_popcount(nx.w[0] & ls.own_mask);
+            }
+            nc = nx;
+        }
+        if (R < S - 1) {
+            xring[R][st & 1][lane] = nc.w[0];
+        } else {
+            const int rr = st - LAG;
+            store_row<1, HH>(orsrc, ls, nc, (rr >= 0 && rr < nrows) ? rr * rowbytes : kOutOfRange);
+        }
+        // hand-off visible to the next wave, and this step's reads done before slots are reused
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
+    using Par0 = std::integral_constant<int, 0>;
+    using Par1 = std::integral_constant<int, 1>;
+    static_for(std::make_integer_sequence<int, FILL>{}, [&](auto stc) {
+        constexpr int ST = decltype(stc)::value;
+        if (ST & 1)
+            step(Par1{}, stc, ST % PL, ST);
+        else
+            step(Par0{}, stc, ST % PL, ST);
+    });
+    for (int s = FILL; s < nsteps; s += PL) {
+#pragma unroll
+        for (int u = 0; u < PL; ++u) {
+            if (u & 1)
+                step(Par1{}, std::integral_constant<int, -1>{}, u, s + u);
+            else
+                step(Par0{}, std::integral_constant<int, -1>{}, u, s + u);
         }
     }
+    if (R == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the ring
+    if (COUNT) flush_counts<NL>(acc, J0, lane, group, slots);
+}
+
+template <int K, bool COUNT, int S>
+__global__ __launch_bounds__(64 * S) void gol_stencil_split(const uint32_t *__restrict__ in,
+                                                            uint32_t *__restrict__ out,
+                                                            StencilParams p,
+                                                            unsigned long long *__restrict__ slots) {
+    static_assert(S >= 2 && K % S == 0, "levels split evenly over S >= 2 waves");
+    __shared__ __attribute__((aligned(16))) uint32_t xring[S - 1][2][64];
+    __shared__ __attribute__((aligned(16))) uint32_t ring[8][64];
+    const int64_t group = blockIdx.x;
+    if (group / p.nchunks >= p.nbands) return;  // whole workgroup
+    const int lane = threadIdx.x & 63;
+    const int r = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    static_for(std::make_integer_sequence<int, S>{}, [&](auto rc) {
+        constexpr int RR = decltype(rc)::value;
+        if (r == RR) split_role<K, COUNT, S, RR>(in, out, p, slots, group, lane, xring, ring);
+    });
 }
 
 // Per-generation counts of a launch whose slots were not finalized in-kernel: block j sums
@@ -718,7 +882,39 @@ const void *variant_fn(int variant) {
     }
 }
 
+template <int K, int S>
+hipError_t launch_split_ks(const uint32_t *in, uint32_t *out, const StencilParams &p,
+                           unsigned long long *slots, hipStream_t s) {
+    const unsigned blocks = (unsigned)(p.nbands * (int64_t)p.nchunks);
+    if (blocks == 0) return hipSuccess;
+    if (slots)
+        hipLaunchKernelGGL((gol_stencil_split<K, true, S>), dim3(blocks), dim3(64 * S), 0, s, in,
+                           out, p, slots);
+    else
+        hipLaunchKernelGGL((gol_stencil_split<K, false, S>), dim3(blocks), dim3(64 * S), 0, s, in,
+                           out, p, slots);
+    return hipGetLastError();
+}
+
 }  // namespace
+
+bool stencil_split_supported(int K, int S) {
+    if (S == 2) return K == 4 || K == 6 || K == 8 || K == 12 || K == 16 || K == 32;
+    if (S == 4) return K == 4 || K == 8 || K == 12 || K == 16 || K == 32;
+    return false;
+}
+
+hipError_t launch_stencil_split(int K, int S, const uint32_t *in_row0, uint32_t *out_row0,
+                                const StencilParams &p, unsigned long long *slots, hipStream_t s) {
+#define GOL_SPLIT_CASE(KK, SS) \
+    if (K == KK && S == SS) return launch_split_ks<KK, SS>(in_row0, out_row0, p, slots, s);
+    GOL_SPLIT_CASE(4, 2) GOL_SPLIT_CASE(6, 2) GOL_SPLIT_CASE(8, 2) GOL_SPLIT_CASE(12, 2)
+    GOL_SPLIT_CASE(16, 2) GOL_SPLIT_CASE(32, 2)
+    GOL_SPLIT_CASE(4, 4) GOL_SPLIT_CASE(8, 4) GOL_SPLIT_CASE(12, 4) GOL_SPLIT_CASE(16, 4)
+    GOL_SPLIT_CASE(32, 4)
+#undef GOL_SPLIT_CASE
+    return hipErrorInvalidValue;
+}
 
 bool stencil_k_supported(int K) {
     return K == 1 || K == 2 || K == 4 || K == 6 || K == 8 || K == 12 || K == 16 || K == 32;

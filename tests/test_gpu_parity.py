@@ -223,3 +223,35 @@ def test_every_kernel_variant(golhip, oracle, monkeypatch, variant, k):
             out, counts, _, _ = run_engine(golhip, board, turns, k=k, counts=True, band_rows=band)
             assert np.array_equal(out, exp), (variant, k, h, w, band)
             assert np.array_equal(counts.astype(np.int64), exp_counts), (variant, k, h, w, band)
+
+
+@pytest.mark.parametrize("split", [2, 4])
+@pytest.mark.parametrize("k", [4, 6, 8, 16, 32])
+def test_level_split_kernel(golhip, oracle, monkeypatch, split, k):
+    """The level-split stencil (gol_stencil_split: the K levels of a band over S waves of one
+    workgroup, rows handed off through LDS, lockstep barriers) on the shapes that stress wrap,
+    half-word halos, short last bands and band seams, with per-turn counts."""
+    if k % split:
+        pytest.skip("levels must split evenly")
+    monkeypatch.setenv("GOLHIP_SPLIT", str(split))
+    for (h, w) in [(77, 640), (16, 16), (300, 4160), (129, 200)]:
+        rng = np.random.default_rng(h * 7 + w + k + split)
+        board = ((rng.random((h, w)) < 0.4) * 255).astype(np.uint8)
+        turns = 3 * k + 1
+        exp, exp_counts = oracle.packed_run(board, turns)
+        for band in (0, 5):
+            out, counts, _, _ = run_engine(golhip, board, turns, k=k, counts=True, band_rows=band)
+            assert np.array_equal(out, exp), (split, k, h, w, band)
+            assert np.array_equal(counts.astype(np.int64), exp_counts), (split, k, h, w, band)
+
+
+def test_small_board_picks_level_split(golhip, oracle):
+    """configs[1]-sized boards take the level-split path automatically; results unchanged."""
+    words = oracle.init_random(5120, 512, seed=2)
+    with golhip.Engine(5120, 512, k=16) as e:
+        e.load_words(words)
+        counts = e.step(200, counts=True)
+        got = e.store_words()
+    ref_counts = oracle.packed_run_words(words, 200)
+    assert np.array_equal(got, words)
+    assert np.array_equal(counts.astype(np.int64), ref_counts)
