@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 #include <utility>
@@ -380,7 +381,9 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
         // LDS-DMA completion) until its row's DMAs have landed: a step issues D DMAs and NSTORE
         // stores, so after the last DMA for step t this wave issued NSTORE stores of step t and
         // (D + NSTORE) ops for each of the PL-1 steps after it; the wait leaves a margin of 2.
-        constexpr int PL = 8;
+        // deeper ring for K <= 2: steps are short, the launch is HBM-bound and needs more bytes
+        // in flight per CU (16 rows x 256 B x 32 waves)
+        constexpr int PL = K <= 2 ? 16 : 8;
         constexpr int kWait = NSTORE + (D + NSTORE) * (PL - 1) - 2;
         static_assert(kWait <= 63, "vmcnt field");
         __shared__ __attribute__((aligned(16))) uint32_t ring[4][PL][64 * D];
@@ -687,15 +690,20 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
     return v;
 }
 
+// Alive cells of rows x wd words (wd % 4 == 0: the torus width is a multiple of 128): a block
+// per row at a time, 16-byte loads, no per-element index division.
 __global__ void popcount_rows(const uint32_t *__restrict__ row0, int64_t pitch, int64_t rows,
                               int32_t wd, unsigned long long *__restrict__ out) {
     __shared__ unsigned long long part[4];
-    const int64_t n = rows * wd;
+    const int q = wd / 4;
     unsigned long long c = 0;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t y = i / wd;
-        c += __builtin_popcount(row0[y * pitch + (i - y * wd)]);
+    for (int64_t y = blockIdx.x; y < rows; y += gridDim.x) {
+        const uint4 *r = reinterpret_cast<const uint4 *>(row0 + y * pitch);
+        for (int i = threadIdx.x; i < q; i += blockDim.x) {
+            const uint4 v = r[i];
+            c += __builtin_popcount(v.x) + __builtin_popcount(v.y) + __builtin_popcount(v.z) +
+                 __builtin_popcount(v.w);
+        }
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
@@ -986,8 +994,8 @@ hipError_t launch_init_random(uint32_t *row0, int64_t pitch, int64_t rows, int64
 
 hipError_t launch_popcount(const uint32_t *row0, int64_t pitch, int64_t rows, int32_t wd,
                            unsigned long long *out, hipStream_t s) {
-    hipLaunchKernelGGL(popcount_rows, dim3(grid_for(rows * wd, 256, 4096)), dim3(256), 0, s, row0,
-                       pitch, rows, wd, out);
+    const unsigned blocks = (unsigned)std::min<int64_t>(std::max<int64_t>(rows, 1), 4096);
+    hipLaunchKernelGGL(popcount_rows, dim3(blocks), dim3(256), 0, s, row0, pitch, rows, wd, out);
     return hipGetLastError();
 }
 
