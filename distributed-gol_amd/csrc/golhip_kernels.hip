@@ -52,13 +52,27 @@ struct Words {
     uint32_t w[D];
 };
 
+// Neighbour words of a lane's row: by DPP from lanes -1 / +1 (NoNb), or given (Nb: level 0 reads
+// them next to its own word from the LDS-DMA ring, saving the two cross-lane moves).
+struct NoNb {};
+struct Nb {
+    uint32_t wl, el;  // the word west of the lane's first word, east of its last word
+};
+
 // Horizontal 3-cell sums (west + self + east) of a lane's D words as sum bits s and carries cy.
-// The lane's outer neighbour words come from lanes -1 / +1 by DPP (one per side per row, so
-// D = 2 halves the cross-lane ops per word); the 1-bit shifts are v_alignbit funnel shifts.
-template <int D>
-__device__ __forceinline__ void row_sum3(const Words<D> &c, Words<D> &s, Words<D> &cy) {
-    const uint32_t wl = lane_from_west(c.w[D - 1]);
-    const uint32_t el = lane_from_east(c.w[0]);
+// The lane's outer neighbour words come from lanes -1 / +1 (one per side per row, so D = 2
+// halves the cross-lane ops per word); the 1-bit shifts are v_alignbit funnel shifts.
+template <int D, class N = NoNb>
+__device__ __forceinline__ void row_sum3(const Words<D> &c, Words<D> &s, Words<D> &cy,
+                                         const N &nb = N{}) {
+    uint32_t wl, el;
+    if constexpr (std::is_same_v<N, Nb>) {
+        wl = nb.wl;
+        el = nb.el;
+    } else {
+        wl = lane_from_west(c.w[D - 1]);
+        el = lane_from_east(c.w[0]);
+    }
 #pragma unroll
     for (int d = 0; d < D; ++d) {
         const uint32_t left = d == 0 ? wl : c.w[d - 1];
@@ -97,11 +111,11 @@ struct RowState {
 
 // One level update: `in` is the new row (below), `above`/`mid` the two previous rows of the level.
 // Writes the next generation of `mid` to nx and stores `in`'s state into `above` (now free).
-template <int D>
+template <int D, class N = NoNb>
 __device__ __forceinline__ void level_update(RowState<D> &above, const RowState<D> &mid,
-                                             const Words<D> &in, Words<D> &nx) {
+                                             const Words<D> &in, Words<D> &nx, const N &nb = N{}) {
     Words<D> ns, ncy;
-    row_sum3<D>(in, ns, ncy);
+    row_sum3<D>(in, ns, ncy, nb);
 #pragma unroll
     for (int d = 0; d < D; ++d)
         nx.w[d] = life_next(above.s.w[d], above.cy.w[d], mid.s.w[d], mid.cy.w[d], mid.c.w[d],
@@ -149,9 +163,10 @@ __device__ __forceinline__ void static_for(std::integer_sequence<int, I...>, F &
 
 // Level update without the rule: only ingests the new row's 3-cell sums into the ring (pipeline
 // fill: the level's output would be garbage, but the rows it holds are needed two steps later).
-template <int D>
-__device__ __forceinline__ void level_ingest(RowState<D> &above, const Words<D> &in) {
-    row_sum3<D>(in, above.s, above.cy);
+template <int D, class N = NoNb>
+__device__ __forceinline__ void level_ingest(RowState<D> &above, const Words<D> &in,
+                                             const N &nb = N{}) {
+    row_sum3<D>(in, above.s, above.cy, nb);
     above.c = in;
 }
 
@@ -316,7 +331,7 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
     // Skewed: levels in descending order, level j takes pend[j] (level j-1's output of the
     //   previous step) and its output overwrites pend[j+1] after level j+1 has read it; level j's
     //   output row is ya - K + st - 1 - 2j.
-    auto step = [&](auto par, auto fill, const Words<D> &vin, int st) {
+    auto step = [&](auto par, auto fill, const Words<D> &vin, int st, const auto &nb0) {
         constexpr int PAR = decltype(par)::value;
         constexpr int FST = decltype(fill)::value;  // fill step index (compile time) or -1
         constexpr bool FILL = FST >= 0 && !SKEW;
@@ -326,15 +341,20 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
             const int j = SKEW ? K - 1 - jj : jj;
             const Words<D> lin = SKEW ? (j == 0 ? vin : pend[j]) : nc;
             if (FILL && FST < 2 * j + 2) {  // folds away: FST and (unrolled) j are constants
-                if (FST >= 2 * j) level_ingest<D>(PAR == 0 ? X[j] : Y[j], lin);
+                if (FST >= 2 * j) {
+                    if (j == 0)
+                        level_ingest<D>(PAR == 0 ? X[j] : Y[j], lin, nb0);
+                    else
+                        level_ingest<D>(PAR == 0 ? X[j] : Y[j], lin);
+                }
                 if (j == K - 1) store_row(lin, kOutOfRange);  // keep the per-step store count
                 continue;
             }
             Words<D> nx;
-            if (PAR == 0)
-                level_update<D>(X[j], Y[j], lin, nx);
+            if (j == 0)  // level 0 takes the new row with its given neighbours (if any)
+                level_update<D>(PAR == 0 ? X[j] : Y[j], PAR == 0 ? Y[j] : X[j], lin, nx, nb0);
             else
-                level_update<D>(Y[j], X[j], lin, nx);
+                level_update<D>(PAR == 0 ? X[j] : Y[j], PAR == 0 ? Y[j] : X[j], lin, nx);
             if (COUNT) {
                 const int r = SKEW ? st - K - 1 - 2 * j : st - K - (j + 1);
                 if (r >= 0 && r < nrows) acc[j] += __builtin_popcount(nx.w[0] & own_mask) +
@@ -368,26 +388,30 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
                 const Words<D> vin = buf[u];
                 buf[u] = load_next();
                 if (u & 1)
-                    step(Par1{}, Steady{}, vin, s + u);
+                    step(Par1{}, Steady{}, vin, s + u, NoNb{});
                 else
-                    step(Par0{}, Steady{}, vin, s + u);
+                    step(Par0{}, Steady{}, vin, s + u, NoNb{});
             }
         }
     } else {
         // LDS ring filled by LDS-DMA (global_load_lds): no VGPR destination, so the prefetch
         // distance costs no registers and no register moves.  A row chunk is D DMAs of 64
         // consecutive words (lane L of DMA i fetches word base + 64i + L), read back as the
-        // lane's D consecutive words.  Each step waits (by hand: the compiler does not track
-        // LDS-DMA completion) until its row's DMAs have landed: a step issues D DMAs and NSTORE
-        // stores, so after the last DMA for step t this wave issued NSTORE stores of step t and
-        // (D + NSTORE) ops for each of the PL-1 steps after it; the wait leaves a margin of 2.
-        // deeper ring for K <= 2: steps are short, the launch is HBM-bound and needs more bytes
-        // in flight per CU (16 rows x 256 B x 32 waves)
+        // lane's D consecutive words.  PL slots, PL-1 rows in flight: step st reads slot
+        // st % PL and refills the slot step st-1 read, AFTER an lgkmcnt(0) wait -- a DMA's LDS
+        // write is not ordered with this wave's earlier ds_reads, so a slot is only refilled once
+        // its reads have returned.  Each step waits (by hand: the compiler does not track LDS-DMA
+        // completion) until its row's DMAs have landed: a step issues D DMAs and NSTORE stores,
+        // so after the last DMA for step st-(PL-1) this wave issued NSTORE stores of that step and
+        // (D + NSTORE) ops for each of the PL-2 steps after it; the wait leaves a margin of 2.
+        // Deeper ring for K <= 2: steps are short, the launch is HBM-bound and needs more bytes
+        // in flight per CU.
         constexpr int PL = K <= 2 ? 16 : 8;
-        constexpr int kWait = NSTORE + (D + NSTORE) * (PL - 1) - 2;
+        constexpr int kWait = NSTORE + (D + NSTORE) * (PL - 2) - 2;
         static_assert(kWait <= 63, "vmcnt field");
         __shared__ __attribute__((aligned(16))) uint32_t ring[4][PL][64 * D];
         const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+        const int nb_w = max(lane * D - 1, 0), nb_e = min(lane * D + D, 64 * D - 1);
         int dcol[D];
         {
             const int base = (int)chunk * stride - D;
@@ -409,7 +433,7 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
 #pragma unroll
         for (int d = 0; d < D; ++d) zero.w[d] = 0;
 #pragma unroll
-        for (int u = 0; u < PL; ++u) {
+        for (int u = 0; u < PL - 1; ++u) {
             dma_next(u);
             // dummy (dropped) stores keep the (DMA, stores) cadence; distinct offsets so no
             // dead-store elimination merges them
@@ -417,15 +441,18 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
             asm volatile("" ::: "memory");
         }
         auto one_step = [&](int u, auto fill, int st) {
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kWait) : "memory");
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"(kWait) : "memory");
+            dma_next((u + PL - 1) % PL);
             Words<D> vin;
 #pragma unroll
             for (int d = 0; d < D; ++d) vin.w[d] = ring[w][u][lane * D + d];
-            dma_next(u);
+            // level 0's neighbour words straight from the ring (the row's lanes -1 / +1; the
+            // edge lanes read a clamped, garbage word: they are halo, as with DPP)
+            const Nb nb0{ring[w][u][nb_w], ring[w][u][nb_e]};
             if (st & 1)
-                step(Par1{}, fill, vin, st);
+                step(Par1{}, fill, vin, st, nb0);
             else
-                step(Par0{}, fill, vin, st);
+                step(Par0{}, fill, vin, st, nb0);
         };
         int s = 0;
         // Pipeline fill of the chained levels (2K steps, fully unrolled so every level's
@@ -497,7 +524,7 @@ __device__ __forceinline__ void split_role(const uint32_t *__restrict__ in, uint
     };
     if (R == 0) {
 #pragma unroll
-        for (int u = 0; u < PL; ++u) dma_next(u);
+        for (int u = 0; u < PL - 1; ++u) dma_next(u);
     }
     // One lockstep step: take the input row (DMA ring or the previous wave's hand-off), run this
     // wave's levels (compile-time fill guards when FST >= 0), hand off or store, barrier.
@@ -506,10 +533,11 @@ __device__ __forceinline__ void split_role(const uint32_t *__restrict__ in, uint
         constexpr int FST = decltype(fill)::value;
         Words<1> nc;
         if (R == 0) {
-            // PL-1 younger DMAs after this slot's; margin of 2
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PL - 1 - 2) : "memory");
+            // PL-1 rows in flight: this slot's DMA has PL-2 younger ones (margin of 2); refill
+            // the slot the previous step read (its read returned before that step's barrier)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PL - 2 - 2) : "memory");
+            dma_next((u + PL - 1) % PL);
             nc.w[0] = ring[u][lane];
-            dma_next(u);
         } else {
             nc.w[0] = xring[R - 1][(st - 1) & 1][lane];
         }
