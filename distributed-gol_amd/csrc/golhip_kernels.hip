@@ -477,6 +477,99 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
     if (COUNT) flush_counts<K>(acc, 0, lane, wave, slots);
 }
 
+// ---------------------------------------------------------------- one generation (K = 1)
+// K = 1 is HBM-bound (0.25 B per cell update against ~13 VALU per 32 cells), so it gets its own
+// memory-shaped kernel: a lane holds 4 consecutive words (one 16-byte load / store per row, 1 KiB
+// per wave instruction), a wave covers 256 words with NO halo lanes (one generation needs only
+// the single bit beyond each edge: lanes 0 and 63 load the word outside the wave as a 4-byte side
+// load, which DPP with bound_ctrl off leaves in place at the wave edge), so 65536-wide rows tile
+// into exactly 8 waves.  Rows stream through a register ring P rows deep; the row sums of the
+// row above and of the middle row stay in registers.  Lanes past the torus width hold the
+// wrapped words (the torus continuation), so partial last chunks need no special case; they
+// just do not store.
+template <bool COUNT>
+__global__ __launch_bounds__(256) void gol_step1(const uint32_t *__restrict__ in,
+                                                 uint32_t *__restrict__ out, StencilParams p,
+                                                 unsigned long long *__restrict__ slots) {
+    constexpr int P = 8;
+    const int lane = threadIdx.x & 63;
+    const int64_t wave =
+        (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int64_t chunk = wave % p.nchunks, bandi = wave / p.nchunks;
+    if (bandi >= p.nbands) return;
+    int ya, yb;
+    band_rows(p, bandi, ya, yb);
+    const int base = (int)chunk * 256;
+    const int colraw = base + lane * 4;  // unwrapped index of the lane's first word
+    const int col = colraw % p.wd;       // wd % 4 == 0: the 4 words never straddle the wrap
+    // side word: west of the wave (lane 0), east of it (lane 63); other lanes reload their own
+    // first word (same cache line, no extra traffic) so the load needs no branch
+    const int xcol = lane == 0 ? (base - 1 + p.wd) % p.wd : lane == 63 ? (base + 256) % p.wd : col;
+    const int nrows = yb - ya, nsteps = nrows + 2;
+    const int rowbytes = (int)(p.pitch * 4);
+    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+        out + (int64_t)ya * p.pitch, 0, (yb - ya) * rowbytes, kBufferRsrcWord3);
+    const bool owned = colraw < p.wd;
+    const int off = owned ? col * 4 : kOutOfRange;
+
+    RowStream rows(p, ya - 1);
+    uint4 buf[P];
+    uint32_t xbuf[P];
+    auto load_next = [&](int u) {
+        const uint32_t *r = in + (int64_t)rows.ly * p.pitch;
+        buf[u] = *reinterpret_cast<const uint4 *>(r + col);
+        xbuf[u] = r[xcol];
+        rows.advance();
+    };
+#pragma unroll
+    for (int u = 0; u < P; ++u) load_next(u);
+
+    Words<4> as, acy, ms, mcy, mc;  // row sums of the row above and of the middle row + its cells
+#pragma unroll
+    for (int d = 0; d < 4; ++d) as.w[d] = acy.w[d] = ms.w[d] = mcy.w[d] = mc.w[d] = 0;
+    uint32_t acc = 0;
+    for (int s = 0; s < nsteps; s += P) {
+#pragma unroll
+        for (int u = 0; u < P; ++u) {
+            const int st = s + u;
+            Words<4> c;
+            c.w[0] = buf[u].x;
+            c.w[1] = buf[u].y;
+            c.w[2] = buf[u].z;
+            c.w[3] = buf[u].w;
+            const uint32_t x = xbuf[u];
+            load_next(u);
+            // neighbour words: lane L-1's last word / lane L+1's first word; at the wave edges the
+            // source lane does not exist and the side word x stays (bound_ctrl off keeps `old`)
+            const Nb nb{(uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)c.w[3], 0x138, 0xf, 0xf, false),
+                        (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)c.w[0], 0x130, 0xf, 0xf, false)};
+            Words<4> bs, bcy;
+            row_sum3<4>(c, bs, bcy, nb);
+            Words<4> nx;
+#pragma unroll
+            for (int d = 0; d < 4; ++d)
+                nx.w[d] = life_next(as.w[d], acy.w[d], ms.w[d], mcy.w[d], mc.w[d], bs.w[d], bcy.w[d]);
+            const int r = st - 2;  // the middle row, relative to ya
+            const bool live = r >= 0 && r < nrows;
+            typedef int v4i __attribute__((ext_vector_type(4)));
+            const v4i v = {(int)nx.w[0], (int)nx.w[1], (int)nx.w[2], (int)nx.w[3]};
+            __builtin_amdgcn_raw_buffer_store_b128(v, orsrc, off + (live ? r * rowbytes : kOutOfRange), 0, 0);
+            if (COUNT && live && owned)
+                acc += __builtin_popcount(nx.w[0]) + __builtin_popcount(nx.w[1]) +
+                       __builtin_popcount(nx.w[2]) + __builtin_popcount(nx.w[3]);
+            as = ms;
+            acy = mcy;
+            ms = bs;
+            mcy = bcy;
+            mc = c;
+        }
+    }
+    if (COUNT) {
+        const uint32_t a[1] = {acc};
+        flush_counts<1>(a, 0, lane, wave, slots);
+    }
+}
+
 // ---------------------------------------------------------------- level-split stencil
 // Small boards are latency-bound: a round of minimal bands gives fewer waves than SIMDs, and a
 // lone wave's time is its dependent chain -- band*K level updates (+ the fill), K levels deep
@@ -897,7 +990,19 @@ hipError_t launch_variant(int variant, const uint32_t *in, uint32_t *out, const 
         case kVariantSkewD2: return launch_stencil_k<K, true, 2>(in, out, p, slots, s);
         case kVariantChainD2: return launch_stencil_k<K, false, 2>(in, out, p, slots, s);
         case kVariantSkewLdsPf: return launch_stencil_k<K, true, 1, 1>(in, out, p, slots, s);
-        case kVariantChainLdsPf: return launch_stencil_k<K, false, 1, 1>(in, out, p, slots, s);
+        case kVariantChainLdsPf:
+            if constexpr (K == 1) {  // the production variant's one-generation kernel
+                const unsigned blocks = (unsigned)((p.nbands * (int64_t)p.nchunks + 3) / 4);
+                if (blocks == 0) return hipSuccess;
+                if (slots)
+                    hipLaunchKernelGGL(gol_step1<true>, dim3(blocks), dim3(256), 0, s, in, out, p,
+                                       slots);
+                else
+                    hipLaunchKernelGGL(gol_step1<false>, dim3(blocks), dim3(256), 0, s, in, out, p,
+                                       slots);
+                return hipGetLastError();
+            }
+            return launch_stencil_k<K, false, 1, 1>(in, out, p, slots, s);
         case kVariantSkewLdsD2: return launch_stencil_k<K, true, 2, 1>(in, out, p, slots, s);
         case kVariantChainLdsD2: return launch_stencil_k<K, false, 2, 1>(in, out, p, slots, s);
         default: return launch_stencil_k<K, true, 1>(in, out, p, slots, s);
@@ -911,7 +1016,9 @@ const void *variant_fn(int variant) {
         case kVariantSkewD2: return (const void *)gol_stencil<K, false, true, 2, 0, kHalfHalo<K, 2>>;
         case kVariantChainD2: return (const void *)gol_stencil<K, false, false, 2, 0, kHalfHalo<K, 2>>;
         case kVariantSkewLdsPf: return (const void *)gol_stencil<K, false, true, 1, 1, kHalfHalo<K, 1>>;
-        case kVariantChainLdsPf: return (const void *)gol_stencil<K, false, false, 1, 1, kHalfHalo<K, 1>>;
+        case kVariantChainLdsPf:
+            if constexpr (K == 1) return (const void *)gol_step1<false>;
+            return (const void *)gol_stencil<K, false, false, 1, 1, kHalfHalo<K, 1>>;
         case kVariantSkewLdsD2: return (const void *)gol_stencil<K, false, true, 2, 1, kHalfHalo<K, 2>>;
         case kVariantChainLdsD2: return (const void *)gol_stencil<K, false, false, 2, 1, kHalfHalo<K, 2>>;
         default: return (const void *)gol_stencil<K, false, true, 1, 0, kHalfHalo<K, 1>>;
