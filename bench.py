@@ -226,7 +226,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "kernel": f"gol_stencil<{a.k}>",
+                "kernel": "gol_step1" if a.k == 1 else f"gol_stencil<{a.k}>",
                 "avg_launch_us": round(avg_launch_ms * 1e3, 2),
                 "gens_per_launch": gens_per_launch,
             },

@@ -246,7 +246,11 @@ int64_t auto_band(golhip_t h, int64_t rows_total, int K, int64_t reserve_waves =
     }
     int &wpc = h->waves_per_cu[K][h->variant];
     if (wpc == 0) wpc = golhip::stencil_waves_per_cu(K, h->variant);
-    const int64_t capacity = (int64_t)h->cus * wpc;
+    // The one-generation kernel (K = 1, production variant) is HBM-bound: it runs best with 2
+    // long-streaming waves per SIMD in one round (measured: 2/SIMD 21.9, 4/SIMD 21.1, 1/SIMD
+    // 19.6 TCUPS at 65536^2; uneven rounds lose 10-20 %, profiles/r01_tune_step1.txt).
+    const bool step1 = K == 1 && h->variant == golhip::kVariantChainLdsPf;
+    const int64_t capacity = (int64_t)h->cus * (step1 ? golhip::kStep1WavesPerCu : wpc);
     // Waves = bands x chunks.  At most `slots` bands are resident at once; use the fewest whole
     // rounds of `slots` bands that keep a band <= kMaxBand rows and split the rows evenly over
     // them.  (A band count just above a round would run its few extra waves after the first
@@ -266,7 +270,7 @@ int64_t auto_band(golhip_t h, int64_t rows_total, int K, int64_t reserve_waves =
                       h->variant == golhip::kVariantSkewLdsPf ||
                       h->variant == golhip::kVariantSkewLdsD2;
     const int64_t lag = skew ? 3 * K - 1 : 2 * K;
-    if (band < rows_total) band = std::max<int64_t>(8, (band + lag + 7) / 8 * 8 - lag);
+    if (band < rows_total && !step1) band = std::max<int64_t>(8, (band + lag + 7) / 8 * 8 - lag);
     return band;
 }
 

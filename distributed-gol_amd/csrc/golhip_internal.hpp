@@ -49,6 +49,7 @@ inline int variant_words(int v) {
 }
 // Words of a row owned by one wave of the stencil (its column chunk): 62 lanes x D words, or 63
 // words with the half-word halo (D = 1, K <= 16: lanes 0 and 63 own half a word each).
+constexpr int kStep1WavesPerCu = 8;  // gol_step1 grid: resident waves per CU it is sized for
 inline int chunk_words(int K, int variant) {
     if (K == 1 && variant == kVariantChainLdsPf) return 256;  // gol_step1: 4 words x 64 lanes
     const int d = variant_words(variant);

@@ -487,11 +487,11 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
 // row above and of the middle row stay in registers.  Lanes past the torus width hold the
 // wrapped words (the torus continuation), so partial last chunks need no special case; they
 // just do not store.
-template <bool COUNT>
+// P = rows in flight per wave; NT bit 0 / bit 1 = non-temporal loads / stores (streamed once).
+template <bool COUNT, int P = 8, int NT = 0>
 __global__ __launch_bounds__(256) void gol_step1(const uint32_t *__restrict__ in,
                                                  uint32_t *__restrict__ out, StencilParams p,
                                                  unsigned long long *__restrict__ slots) {
-    constexpr int P = 8;
     const int lane = threadIdx.x & 63;
     const int64_t wave =
         (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -517,8 +517,15 @@ __global__ __launch_bounds__(256) void gol_step1(const uint32_t *__restrict__ in
     uint32_t xbuf[P];
     auto load_next = [&](int u) {
         const uint32_t *r = in + (int64_t)rows.ly * p.pitch;
-        buf[u] = *reinterpret_cast<const uint4 *>(r + col);
-        xbuf[u] = r[xcol];
+        if constexpr (NT & 1) {
+            typedef unsigned v4u __attribute__((ext_vector_type(4)));
+            const v4u t = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(r + col));
+            buf[u] = make_uint4(t.x, t.y, t.z, t.w);
+            xbuf[u] = __builtin_nontemporal_load(r + xcol);
+        } else {
+            buf[u] = *reinterpret_cast<const uint4 *>(r + col);
+            xbuf[u] = r[xcol];
+        }
         rows.advance();
     };
 #pragma unroll
@@ -553,7 +560,8 @@ __global__ __launch_bounds__(256) void gol_step1(const uint32_t *__restrict__ in
             const bool live = r >= 0 && r < nrows;
             typedef int v4i __attribute__((ext_vector_type(4)));
             const v4i v = {(int)nx.w[0], (int)nx.w[1], (int)nx.w[2], (int)nx.w[3]};
-            __builtin_amdgcn_raw_buffer_store_b128(v, orsrc, off + (live ? r * rowbytes : kOutOfRange), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(v, orsrc, off + (live ? r * rowbytes : kOutOfRange), 0,
+                                                   (NT & 2) ? 2 /* nt */ : 0);
             if (COUNT && live && owned)
                 acc += __builtin_popcount(nx.w[0]) + __builtin_popcount(nx.w[1]) +
                        __builtin_popcount(nx.w[2]) + __builtin_popcount(nx.w[3]);
@@ -967,6 +975,49 @@ inline size_t lds_pad_bytes() {
 template <int K, int D>
 constexpr bool kHalfHalo = D == 1 && K <= 16;  // keep in sync with chunk_words()
 
+// Tuning knob GOLHIP_STEP1 = P*10 + NT selects gol_step1's prefetch depth and cache policy
+// (read once; unset = the production configuration).
+inline int step1_config() {
+    static const int cfg = [] {
+        const char *e = std::getenv("GOLHIP_STEP1");
+        return e ? std::atoi(e) : 42;
+    }();
+    return cfg;
+}
+template <int P, int NT>
+hipError_t launch_step1_cfg(const uint32_t *in, uint32_t *out, const StencilParams &p,
+                            unsigned long long *slots, hipStream_t s) {
+    const unsigned blocks = (unsigned)((p.nbands * (int64_t)p.nchunks + 3) / 4);
+    if (blocks == 0) return hipSuccess;
+    if (slots)
+        hipLaunchKernelGGL((gol_step1<true, P, NT>), dim3(blocks), dim3(256), 0, s, in, out, p, slots);
+    else
+        hipLaunchKernelGGL((gol_step1<false, P, NT>), dim3(blocks), dim3(256), 0, s, in, out, p, slots);
+    return hipGetLastError();
+}
+#define GOLHIP_STEP1_CONFIGS(X) \
+    X(20, 2, 0) X(22, 2, 2) X(30, 3, 0) X(32, 3, 2) X(40, 4, 0) X(41, 4, 1) X(42, 4, 2) \
+    X(43, 4, 3) X(60, 6, 0) X(62, 6, 2) X(80, 8, 0) X(82, 8, 2)
+inline hipError_t launch_step1(const uint32_t *in, uint32_t *out, const StencilParams &p,
+                               unsigned long long *slots, hipStream_t s) {
+    switch (step1_config()) {
+#define GOLHIP_X(C, P, NT) \
+    case C: return launch_step1_cfg<P, NT>(in, out, p, slots, s);
+        GOLHIP_STEP1_CONFIGS(GOLHIP_X)
+#undef GOLHIP_X
+        default: return launch_step1_cfg<4, 2>(in, out, p, slots, s);
+    }
+}
+inline const void *step1_fn() {
+    switch (step1_config()) {
+#define GOLHIP_X(C, P, NT) \
+    case C: return (const void *)gol_step1<false, P, NT>;
+        GOLHIP_STEP1_CONFIGS(GOLHIP_X)
+#undef GOLHIP_X
+        default: return (const void *)gol_step1<false, 4, 2>;
+    }
+}
+
 template <int K, bool SKEW, int D, int PF = 0>
 hipError_t launch_stencil_k(const uint32_t *in, uint32_t *out, const StencilParams &p,
                             unsigned long long *slots, hipStream_t s) {
@@ -991,17 +1042,7 @@ hipError_t launch_variant(int variant, const uint32_t *in, uint32_t *out, const 
         case kVariantChainD2: return launch_stencil_k<K, false, 2>(in, out, p, slots, s);
         case kVariantSkewLdsPf: return launch_stencil_k<K, true, 1, 1>(in, out, p, slots, s);
         case kVariantChainLdsPf:
-            if constexpr (K == 1) {  // the production variant's one-generation kernel
-                const unsigned blocks = (unsigned)((p.nbands * (int64_t)p.nchunks + 3) / 4);
-                if (blocks == 0) return hipSuccess;
-                if (slots)
-                    hipLaunchKernelGGL(gol_step1<true>, dim3(blocks), dim3(256), 0, s, in, out, p,
-                                       slots);
-                else
-                    hipLaunchKernelGGL(gol_step1<false>, dim3(blocks), dim3(256), 0, s, in, out, p,
-                                       slots);
-                return hipGetLastError();
-            }
+            if constexpr (K == 1) return launch_step1(in, out, p, slots, s);  // production K = 1
             return launch_stencil_k<K, false, 1, 1>(in, out, p, slots, s);
         case kVariantSkewLdsD2: return launch_stencil_k<K, true, 2, 1>(in, out, p, slots, s);
         case kVariantChainLdsD2: return launch_stencil_k<K, false, 2, 1>(in, out, p, slots, s);
@@ -1017,7 +1058,7 @@ const void *variant_fn(int variant) {
         case kVariantChainD2: return (const void *)gol_stencil<K, false, false, 2, 0, kHalfHalo<K, 2>>;
         case kVariantSkewLdsPf: return (const void *)gol_stencil<K, false, true, 1, 1, kHalfHalo<K, 1>>;
         case kVariantChainLdsPf:
-            if constexpr (K == 1) return (const void *)gol_step1<false>;
+            if constexpr (K == 1) return step1_fn();
             return (const void *)gol_stencil<K, false, false, 1, 1, kHalfHalo<K, 1>>;
         case kVariantSkewLdsD2: return (const void *)gol_stencil<K, false, true, 2, 1, kHalfHalo<K, 2>>;
         case kVariantChainLdsD2: return (const void *)gol_stencil<K, false, false, 2, 1, kHalfHalo<K, 2>>;

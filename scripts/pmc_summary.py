@@ -27,7 +27,7 @@ def main():
     per = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> values per dispatch
     for r in load(d):
         name = r.get("Kernel_Name", "")
-        short = ("stencil" if "gol_stencil" in name else "popcount" if "popcount_rows" in name
+        short = ("stencil" if ("gol_stencil" in name or "gol_step1" in name) else "popcount" if "popcount_rows" in name
                  else "init" if "init_random" in name else None)
         if short:
             per[short][r["Counter_Name"]].append(float(r["Counter_Value"]))

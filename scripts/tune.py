@@ -30,7 +30,7 @@ for rnd in range(3):
             for b in bands:
                 e.set_k(k)
                 e.set_band_rows(b)
-                n = max(32, 4 * k)
+                n = max(int(os.environ.get("TUNE_STEPS", "32")), 4 * k)
                 e.step(k)
                 e.sync()
                 t = time.perf_counter()
