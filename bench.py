@@ -17,7 +17,10 @@ Prints ONE JSON line on rank 0 (keys per the driver contract), plus:
                  (13 per 32-cell word per generation) per second vs the issue peak of that mix;
   cpu_baseline : the reference algorithm (oracle/ port of server/server.go + broker split,
                  byte per cell, 4 servers x T threads) timed on this host on a bounded sample;
-  k_sweep      : GCUPS per temporal-blocking depth k (N == 1 only).
+  k_sweep      : GCUPS per temporal-blocking depth k (N == 1 only);
+  hbm_roofline_k1: the k = 1 kernel (gol_step1, no temporal reuse) against the HBM peak;
+  strong_262144: configs[3] -- the 262144^2 board (seed 4) split over the N ranks, GCUPS and
+                 GCUPS per GPU (strong scaling of one fixed board; --no-strong skips it).
 """
 from __future__ import annotations
 
@@ -66,6 +69,10 @@ def parse():
     ap.add_argument("--no-timing", action="store_true",
                     help="no per-launch HIP events in the timed region (roofline from wall time)")
     ap.add_argument("--pmc-file", default=str(ROOT / "profiles" / "pmc_traffic.json"))
+    ap.add_argument("--no-strong", action="store_true",
+                    help="skip the configs[3] leg (262144^2 board split over the N ranks)")
+    ap.add_argument("--strong-size", type=int, default=262144)
+    ap.add_argument("--strong-steps", type=int, default=160)
     return ap.parse_args()
 
 
@@ -137,7 +144,8 @@ def main():
     if a.band_rows:
         eng.set_band_rows(a.band_rows)
     eng.init_random(a.seed)
-    local_cells = eng.info.rows * width
+    local_rows = eng.info.rows
+    local_cells = local_rows * width
 
     eng.step(a.warmup)
     eng.sync()
@@ -183,18 +191,51 @@ def main():
         pass
 
     sweep = None
+    k1_launch_us = None
     if world == 1 and not a.no_sweep:
         sweep = {}
         for kk in (1, 2, 4, 8, 16, 32):
             eng.set_k(kk)
-            eng.step(2 * kk)
-            n = max(4 * kk, 32)
+            # the first ~250 one-generation launches of a process run ~10 % slower (measured,
+            # scripts/diag_k1.py), so k = 1 gets a longer untimed warmup
+            eng.step(256 if kk == 1 else 2 * kk)
+            n = max(4 * kk, 256)
+            eng.timing(kk == 1)
             t = timed_steps(eng, n, 1)
+            if kk == 1:
+                ms1, l1, _ = eng.kernel_time()
+                k1_launch_us = ms1 * 1e3 / max(l1, 1)
+                eng.timing(False)
             sweep[str(kk)] = round(width * height * n / t / 1e9, 1)
         eng.set_k(a.k)
 
     checksum = eng.alive_count()  # collective
     eng.close()
+    del eng
+
+    # configs[3]: the 262144^2 board (seed 4) row-strip sharded over the N ranks (strong scaling
+    # of a fixed board; per-GPU rate comparable across N), RCCL halos when N > 1
+    strong = None
+    if not a.no_strong:
+        n = a.strong_size
+        sid = None
+        if world > 1:  # a fresh RCCL unique id per communicator
+            obj = [golhip.nccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            sid = obj[0]
+        se = golhip.Engine(n, n, k=a.k, rank=rank, world_size=world, device=local, nccl_id=sid)
+        se.init_random(4)
+        se.step(a.k)
+        se.sync()
+        t = timed_steps(se, a.strong_steps, world)
+        strong_alive = se.alive_count()  # collective
+        se.close()
+        del se
+        g = n * n * a.strong_steps / t / 1e9
+        strong = {"board": f"{n}x{n}", "seed": 4, "steps": a.strong_steps, "k": a.k,
+                  "rows_per_gpu": -(-n // world), "gcups": round(g, 1),
+                  "gcups_per_gpu": round(g / world, 1), "ms_per_step": round(t * 1e3 / a.strong_steps, 4),
+                  "alive_after": int(strong_alive)}
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
@@ -216,7 +257,7 @@ def main():
             "data": "synthetic (counter-based splitmix64 random board, p=0.5, generated on device)",
             "config": {
                 "workload": (f"{width}x{height} torus, random p=0.5 seed {a.seed}, "
-                             f"{world} row strip(s) of {eng.info.rows} rows, k={a.k} gens/launch"),
+                             f"{world} row strip(s) of {local_rows} rows, k={a.k} gens/launch"),
                 "width": width, "height": height, "k": a.k, "parallelism": f"rows{world}",
             },
             "roofline": {
@@ -233,6 +274,16 @@ def main():
             "valu_roofline": valu,
             "cpu_baseline": cpu,
             "k_sweep_gcups": sweep,
+            # the north star's HBM figure for the one-generation kernel (no temporal reuse):
+            # k = 1 sweep rate x 0.25 B per cell-update vs the 8 TB/s peak
+            # (algorithmic bytes of one launch over its HIP-event duration, as for "roofline")
+            "hbm_roofline_k1": None if not k1_launch_us else {
+                "kernel": "gol_step1", "gcups_wall": sweep["1"],
+                "avg_launch_us": round(k1_launch_us, 2),
+                "achieved": round(BYTES_PER_CELL_UPDATE * local_cells / k1_launch_us / 1e3, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(BYTES_PER_CELL_UPDATE * local_cells / k1_launch_us / 1e3 / HBM_PEAK_GBS, 4)},
+            "strong_262144": strong,
             "alive_after_timed": int(alive_timed),
             "alive_after": int(checksum),
         }
