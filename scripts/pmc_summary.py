@@ -44,6 +44,12 @@ def main():
                     "algorithmic_bytes_per_launch": 0.25 * board * 8 * k})
     except KeyError as e:
         out["error"] = f"missing {e}"
+    st = avg.get("stencil", {})
+    if "SQ_LDS_BANK_CONFLICT" in st and st.get("SQ_LDS_IDX_ACTIVE"):
+        # extra LDS cycles from bank conflicts over all LDS-array cycles (MI355X_MICROARCH.md)
+        out["lds_bank_conflict_cycles"] = st["SQ_LDS_BANK_CONFLICT"]
+        out["lds_active_cycles"] = st["SQ_LDS_IDX_ACTIVE"]
+        out["lds_bank_conflict_frac"] = st["SQ_LDS_BANK_CONFLICT"] / st["SQ_LDS_IDX_ACTIVE"]
     print(json.dumps(out, indent=1))
     if len(sys.argv) > 5:
         try:
