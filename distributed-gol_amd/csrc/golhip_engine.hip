@@ -30,6 +30,7 @@ using golhip::StencilParams;
 namespace {
 
 constexpr int kVersion = 100;
+constexpr int kCountWindow = 4096;  // generations of per-turn counts finalized per launch
 
 struct Shard {
     int device = 0;
@@ -39,7 +40,7 @@ struct Shard {
     hipStream_t edge = nullptr;  // boundary bands of a split board, concurrent with the interior
     hipEvent_t ev_ready = nullptr, ev_halo = nullptr, ev_edge = nullptr;
     uint32_t *buf[2] = {nullptr, nullptr};  // allocation base (halo rows first)
-    unsigned long long *slots = nullptr;    // kMaxK * kCountSlots
+    unsigned long long *slots = nullptr;    // kCountWindow * kCountSlots (count window)
     unsigned long long *scratch_u64 = nullptr;
     unsigned long long *d_counts = nullptr;
     size_t d_counts_cap = 0;
@@ -157,9 +158,9 @@ int alloc_shard(golhip_t h, Shard &s) {
         HIPCHK(h, hipMalloc(&s.buf[i], words * sizeof(uint32_t)));
         HIPCHK(h, hipMemsetAsync(s.buf[i], 0, words * sizeof(uint32_t), s.compute));
     }
-    HIPCHK(h, hipMalloc(&s.slots, sizeof(unsigned long long) * golhip::kMaxK * golhip::kCountSlots));
+    HIPCHK(h, hipMalloc(&s.slots, sizeof(unsigned long long) * kCountWindow * golhip::kCountSlots));
     HIPCHK(h, hipMemsetAsync(s.slots, 0,
-                             sizeof(unsigned long long) * golhip::kMaxK * golhip::kCountSlots,
+                             sizeof(unsigned long long) * kCountWindow * golhip::kCountSlots,
                              s.compute));
     HIPCHK(h, hipMalloc(&s.scratch_u64, sizeof(unsigned long long) * 4));
     HIPCHK(h, hipStreamSynchronize(s.compute));
@@ -415,8 +416,9 @@ int exchange_halos(golhip_t h, int K) {
     return GOLHIP_OK;
 }
 
-// One K-generation block on every shard. counts_dev_off: index into s.d_counts (or -1).
-int step_block(golhip_t h, int K, int64_t counts_off) {
+// One K-generation block on every shard.  slot_gen >= 0: count the K generations into the count
+// window at generation slot_gen (finalized later by flush_counts_window), -1: no counts.
+int step_block(golhip_t h, int K, int64_t slot_gen) {
     if (h->split) {
         int rc = exchange_halos(h, K);
         if (rc) return rc;
@@ -424,7 +426,8 @@ int step_block(golhip_t h, int K, int64_t counts_off) {
     const int nxt = h->cur ^ 1;
     for (auto &s : h->shards) {
         HIPCHK(h, hipSetDevice(s.device));
-        unsigned long long *slots = counts_off >= 0 ? s.slots : nullptr;
+        unsigned long long *slots =
+            slot_gen >= 0 ? s.slots + slot_gen * golhip::kCountSlots : nullptr;
         const uint32_t *in = h->row0(s, h->cur);
         uint32_t *out = h->row0(s, nxt);
         if (!h->split) {
@@ -448,9 +451,6 @@ int step_block(golhip_t h, int K, int64_t counts_off) {
             StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0);
             HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, p, slots, s.compute));
         }
-        if (counts_off >= 0)
-            HIPCHK(h, golhip::launch_count_finalize(K, s.slots, s.d_counts + counts_off,
-                                                     s.compute));
     }
     if (h->timing) {
         h->tlaunches += 1;
@@ -459,6 +459,17 @@ int step_block(golhip_t h, int K, int64_t counts_off) {
     h->cur = nxt;
     h->turn += K;
     h->prev_valid = (K == 1);
+    return GOLHIP_OK;
+}
+
+// Per-generation counts of the first n window generations -> s.d_counts[off, off + n), one
+// finalize launch per window (it re-zeroes the slots) instead of one per K-generation block.
+int flush_counts_window(golhip_t h, int n, int64_t off) {
+    if (n <= 0) return GOLHIP_OK;
+    for (auto &s : h->shards) {
+        HIPCHK(h, hipSetDevice(s.device));
+        HIPCHK(h, golhip::launch_count_finalize(n, s.slots, s.d_counts + off, s.compute));
+    }
     return GOLHIP_OK;
 }
 
@@ -602,7 +613,7 @@ int create_common(golhip_t h) {
     return GOLHIP_OK;
 }
 
-constexpr int kGraphGens = 128;  // generations per graph replay
+constexpr int kGraphGens = 128;  // generations per graph replay (<= kCountWindow)
 
 // Graphs pay off when a launch is short (launch-bound): < ~100 us of stencil work.
 bool graph_worthy(golhip_t h, int K) {
@@ -629,11 +640,11 @@ int graph_for(golhip_t h, int K, int M, bool counting, hipGraphExec_t *out) {
         const int c = h->cur ^ (i & 1);
         StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0);
         err = launch_auto(h, K, h->row0(s, c), h->row0(s, c ^ 1), p,
-                          counting ? s.slots : nullptr, s.compute);
-        if (err == hipSuccess && counting)
-            err = golhip::launch_count_finalize(K, s.slots, h->g_counts + (int64_t)i * K,
-                                                s.compute);
+                          counting ? s.slots + (int64_t)i * K * golhip::kCountSlots : nullptr,
+                          s.compute);
     }
+    if (err == hipSuccess && counting)  // one finalize for the graph's M*K generations
+        err = golhip::launch_count_finalize(M * K, s.slots, h->g_counts, s.compute);
     hipError_t e2 = hipStreamEndCapture(s.compute, &graph);
     if (err != hipSuccess || e2 != hipSuccess)
         return fail(h, GOLHIP_ERR_HIP, "graph capture: %s", hipGetErrorString(err ? err : e2));
@@ -945,9 +956,15 @@ int golhip_step(golhip_t h, int64_t turns, uint64_t *alive_per_turn) {
     const int Kfull = pick_k(h->k);
     const int M = std::max(2, (kGraphGens / Kfull) & ~1);
     const bool graphs = graph_worthy(h, Kfull) && turns >= (int64_t)M * Kfull;
+    int64_t win = 0;  // generations pending in the count window, from turn offset done - win
     while (done < turns) {
         const int64_t left = turns - done;
         if (graphs && left >= (int64_t)M * Kfull) {
+            if (counting) {  // the graph finalizes its own generations from window slot 0
+                int rc = flush_counts_window(h, (int)win, done - win);
+                if (rc) return rc;
+                win = 0;
+            }
             hipGraphExec_t exec = nullptr;
             int rc = graph_for(h, Kfull, M, counting, &exec);
             if (rc) return rc;
@@ -967,9 +984,19 @@ int golhip_step(golhip_t h, int64_t turns, uint64_t *alive_per_turn) {
             continue;
         }
         const int K = pick_k((int)std::min<int64_t>(left, h->k));
-        int rc = step_block(h, K, counting ? done : -1);
+        if (counting && win + K > kCountWindow) {
+            int rc = flush_counts_window(h, (int)win, done - win);
+            if (rc) return rc;
+            win = 0;
+        }
+        int rc = step_block(h, K, counting ? win : -1);
         if (rc) return rc;
         done += K;
+        if (counting) win += K;
+    }
+    if (counting) {
+        int rc = flush_counts_window(h, (int)win, done - win);
+        if (rc) return rc;
     }
     if (stop) {
         HIPCHK(h, hipSetDevice(h->shards[0].device));
