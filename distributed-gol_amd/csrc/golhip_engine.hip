@@ -14,6 +14,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -252,27 +253,58 @@ int64_t auto_band(golhip_t h, int64_t rows_total, int K, int64_t reserve_waves =
     // 19.6 TCUPS at 65536^2; uneven rounds lose 10-20 %, profiles/r01_tune_step1.txt).
     const bool step1 = K == 1 && h->variant == golhip::kVariantChainLdsPf;
     const int64_t capacity = (int64_t)h->cus * (step1 ? golhip::kStep1WavesPerCu : wpc);
-    // Waves = bands x chunks.  At most `slots` bands are resident at once; use the fewest whole
-    // rounds of `slots` bands that keep a band <= kMaxBand rows and split the rows evenly over
-    // them.  (A band count just above a round would run its few extra waves after the first
-    // round: a tail as long as a whole band with the chip nearly idle.)
     constexpr int64_t kMaxBand = 4096;
-    const int64_t slots = std::max<int64_t>(1, (capacity - reserve_waves) / nchunks);
-    const int64_t rounds = (rows_total + slots * kMaxBand - 1) / (slots * kMaxBand);
-    int64_t band = (rows_total + rounds * slots - 1) / (rounds * slots);
+    const bool skew = h->variant == golhip::kVariantSkew || h->variant == golhip::kVariantSkewD2 ||
+                      h->variant == golhip::kVariantSkewLdsPf ||
+                      h->variant == golhip::kVariantSkewLdsD2;
+    const int64_t lag = skew ? 3 * K - 1 : 2 * K;
+    // A wave runs band + lag steps in blocks of 8 (the kernel's prefetch ring); bands are rounded
+    // so that full bands end on a block boundary instead of computing up to 7 discarded rows.
+    auto aligned = [&](int64_t b) {
+        return step1 ? b : std::max<int64_t>(8, (b + lag + 7) / 8 * 8 - lag);
+    };
+    int64_t band;
+    if (step1) {
+        // Waves = bands x chunks.  At most `slots` bands are resident at once; use the fewest
+        // whole rounds of `slots` bands that keep a band <= kMaxBand rows and split the rows
+        // evenly over them.
+        const int64_t slots = std::max<int64_t>(1, (capacity - reserve_waves) / nchunks);
+        const int64_t rounds = (rows_total + slots * kMaxBand - 1) / (slots * kMaxBand);
+        band = (rows_total + rounds * slots - 1) / (rounds * slots);
+    } else {
+        // K >= 2 (VALU-bound): bands x chunks come to just under an integer m waves per SIMD
+        // (a remainder band counting by its length), m from two to four rounds of residency,
+        // choosing the m with the least modelled time m x (band + K) (K ~ a wave's pipeline-fill
+        // cost in rows).  Measured (profiles/r01_tune_band16.txt): GCUPS follows a sawtooth of
+        // period one wave per SIMD -- at 65536^2, k = 16: 111.7 at band 264 (8.0 waves/SIMD),
+        // 103.2 at band 256 (8.2), 106.5 at one round (band 528); at 262144^2 the waves just over
+        // a multiple lose 5-10 % the same way.
+        const int64_t simds = 4 * (int64_t)h->cus;  // gfx9: 4 SIMDs per CU
+        const int64_t m0 = std::max<int64_t>(2, 2 * (int64_t)wpc / 4);
+        const double work = (double)rows_total * (double)nchunks;
+        // Among m within 1 % of the least cost take the largest (more, shorter bands measured
+        // 3 % faster at 262144^2: band 2232 vs 3728).
+        std::vector<std::pair<int64_t, double>> cand;  // (band, cost) per m
+        for (int64_t m = m0; m <= 2 * m0 || cand.empty(); ++m) {
+            const double slots = (double)(m * simds - reserve_waves);
+            if (slots <= 0) continue;
+            const int64_t b = aligned(std::max<int64_t>(1, (int64_t)std::ceil(work / slots)));
+            if (b > kMaxBand && m < 64) continue;
+            cand.push_back({b, (double)m * (double)(b + K)});
+        }
+        double best = cand[0].second;
+        for (auto &c : cand) best = std::min(best, c.second);
+        band = cand[0].first;
+        for (auto &c : cand)
+            if (c.second <= 1.01 * best) band = c.first;
+    }
     // Small boards (fewer rows than a round of minimal bands) are latency-bound: a wave's work is
     // band*K level updates plus the K(K-1) of its pipeline fill, so bands shorter than K mostly
     // add fill; K-row bands measured best (profiles/r01_tune_small_*).
     band = std::max<int64_t>(band, std::min<int64_t>(std::max(K, 8), rows_total));
     band = std::max<int64_t>(band, 1);
-    // A wave runs band + lag steps in blocks of 8 (the kernel's prefetch ring); round the band so
-    // that full bands end on a block boundary instead of computing up to 7 discarded rows.
-    const bool skew = h->variant == golhip::kVariantSkew || h->variant == golhip::kVariantSkewD2 ||
-                      h->variant == golhip::kVariantSkewLdsPf ||
-                      h->variant == golhip::kVariantSkewLdsD2;
-    const int64_t lag = skew ? 3 * K - 1 : 2 * K;
-    if (band < rows_total && !step1) band = std::max<int64_t>(8, (band + lag + 7) / 8 * 8 - lag);
-    return band;
+    if (band < rows_total) band = aligned(band);
+    return std::min(band, std::max<int64_t>(rows_total, 1));
 }
 
 // Waves per (band, chunk) of a launch over rows_total rows: the level-split kernel (S = 2 or 4)
