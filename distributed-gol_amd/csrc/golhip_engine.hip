@@ -31,7 +31,13 @@ using golhip::StencilParams;
 namespace {
 
 constexpr int kVersion = 100;
-constexpr int kCountWindow = 4096;  // generations of per-turn counts finalized per launch
+// Generations of per-turn counts finalized per launch (GOLHIP_COUNT_WINDOW, read at create,
+// overrides it; at least the graph length kGraphGens: tests shrink it to exercise flushes).
+int count_window_env() {
+    const char *e = std::getenv("GOLHIP_COUNT_WINDOW");
+    const int v = e ? std::atoi(e) : 4096;
+    return v < 128 ? 128 : v;
+}
 
 struct Shard {
     int device = 0;
@@ -41,7 +47,7 @@ struct Shard {
     hipStream_t edge = nullptr;  // boundary bands of a split board, concurrent with the interior
     hipEvent_t ev_ready = nullptr, ev_halo = nullptr, ev_edge = nullptr;
     uint32_t *buf[2] = {nullptr, nullptr};  // allocation base (halo rows first)
-    unsigned long long *slots = nullptr;    // kCountWindow * kCountSlots (count window)
+    unsigned long long *slots = nullptr;    // count_window x kCountSlots
     unsigned long long *scratch_u64 = nullptr;
     unsigned long long *d_counts = nullptr;
     size_t d_counts_cap = 0;
@@ -69,6 +75,7 @@ struct golhip_engine {
     int32_t wd = 0;
     int world_size = 1;
     int k = 1, halo = 0, band_rows = 0;
+    int count_window = 4096;  // generations per count-window finalize
     int variant = golhip::kVariantChainLdsPf;  // fastest measured (profiles/r01_tune_*)
     int cus = 0;                 // compute units of the first device (grid sizing)
     int waves_per_cu[golhip::kMaxK + 1][golhip::kNumVariants] = {};  // occupancy cache per (K, variant)
@@ -159,9 +166,9 @@ int alloc_shard(golhip_t h, Shard &s) {
         HIPCHK(h, hipMalloc(&s.buf[i], words * sizeof(uint32_t)));
         HIPCHK(h, hipMemsetAsync(s.buf[i], 0, words * sizeof(uint32_t), s.compute));
     }
-    HIPCHK(h, hipMalloc(&s.slots, sizeof(unsigned long long) * kCountWindow * golhip::kCountSlots));
+    HIPCHK(h, hipMalloc(&s.slots, sizeof(unsigned long long) * h->count_window * golhip::kCountSlots));
     HIPCHK(h, hipMemsetAsync(s.slots, 0,
-                             sizeof(unsigned long long) * kCountWindow * golhip::kCountSlots,
+                             sizeof(unsigned long long) * h->count_window * golhip::kCountSlots,
                              s.compute));
     HIPCHK(h, hipMalloc(&s.scratch_u64, sizeof(unsigned long long) * 4));
     HIPCHK(h, hipStreamSynchronize(s.compute));
@@ -208,6 +215,7 @@ int setup_engine(golhip_t h, int width, int height, int world, int k) {
     h->split = world > 1;
     h->halo = h->split ? k : 0;
     if (const char *e = std::getenv("GOLHIP_BAND_ROWS")) h->band_rows = std::atoi(e);
+    h->count_window = count_window_env();
     if (const char *e = std::getenv("GOLHIP_SPLIT")) h->force_split = std::atoi(e);
     if (const char *e = std::getenv("GOLHIP_VARIANT"))
         h->variant = std::strcmp(e, "chain") == 0     ? golhip::kVariantChain
@@ -645,7 +653,7 @@ int create_common(golhip_t h) {
     return GOLHIP_OK;
 }
 
-constexpr int kGraphGens = 128;  // generations per graph replay (<= kCountWindow)
+constexpr int kGraphGens = 128;  // generations per graph replay (<= count_window)
 
 // Graphs pay off when a launch is short (launch-bound): < ~100 us of stencil work.
 bool graph_worthy(golhip_t h, int K) {
@@ -1016,7 +1024,7 @@ int golhip_step(golhip_t h, int64_t turns, uint64_t *alive_per_turn) {
             continue;
         }
         const int K = pick_k((int)std::min<int64_t>(left, h->k));
-        if (counting && win + K > kCountWindow) {
+        if (counting && win + K > h->count_window) {
             int rc = flush_counts_window(h, (int)win, done - win);
             if (rc) return rc;
             win = 0;

@@ -255,3 +255,21 @@ def test_small_board_picks_level_split(golhip, oracle):
     ref_counts = oracle.packed_run_words(words, 200)
     assert np.array_equal(got, words)
     assert np.array_equal(counts.astype(np.int64), ref_counts)
+
+
+@pytest.mark.parametrize("k", [6, 16])
+def test_count_window_flushes(golhip, oracle, monkeypatch, k):
+    """Per-turn counts go through a count window finalized once per window: with the window at
+    its 128-generation minimum and graphs off, a 700-turn call flushes it several times (K = 6
+    does not divide it); every count must equal the oracle's and the board must match."""
+    monkeypatch.setenv("GOLHIP_COUNT_WINDOW", "128")
+    monkeypatch.setenv("GOLHIP_GRAPHS", "0")
+    w, h = 640, 200
+    board = oracle.unpack(oracle.init_random(640, h, seed=11), w)
+    with golhip.Engine(w, h, k=k) as e:
+        e.load(board)
+        c = e.step(700, counts=True)
+        got = e.store()
+    exp, exp_counts = oracle.packed_run(board, 700)
+    assert np.array_equal(got, exp)
+    assert np.array_equal(c.astype(np.int64), exp_counts)  # exp_counts[i]: after turn i + 1
