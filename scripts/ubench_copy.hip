@@ -32,6 +32,48 @@ __global__ __launch_bounds__(256) void copy_rows(const v4u *__restrict__ in, v4u
     }
 }
 
+// Linear grid-stride float4 copy (the classic streaming copy) for comparison.
+template <int NT>
+__global__ __launch_bounds__(256) void copy_linear(const v4u *__restrict__ in, v4u *__restrict__ out,
+                                                   int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        v4u v = in[i];
+        if (NT) __builtin_nontemporal_store(v, out + i);
+        else out[i] = v;
+    }
+}
+template <int NT, int U>
+__global__ __launch_bounds__(256) void copy_linear_u(const v4u *__restrict__ in, v4u *__restrict__ out,
+                                                     int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride * U) {
+        v4u v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = in[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (NT) __builtin_nontemporal_store(v[u], out + i + u * stride);
+            else out[i + u * stride] = v[u];
+        }
+    }
+}
+template <class F>
+void time_it(const char *name, F f) {
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    for (int i = 0; i < 3; ++i) f();
+    (void)hipEventRecord(a);
+    const int it = 50;
+    for (int i = 0; i < it; ++i) f();
+    (void)hipEventRecord(b);
+    (void)hipEventSynchronize(b);
+    float ms;
+    (void)hipEventElapsedTime(&ms, a, b);
+    const double t = ms / 1e3 / it;
+    printf("%s: %.1f us  %.0f GB/s\n", name, t * 1e6, 2.0 * kRows * kRowWords * 4 / t / 1e9);
+}
+
 template <int P, int NT>
 void run(const v4u *in, v4u *out, int wpc, int cus) {
     const int waves = wpc * cus;
@@ -60,6 +102,16 @@ int main() {
     hipMalloc(&out, bytes);
     hipMemset(in, 0x5a, bytes);
     int cus = 256;
+    const int64_t n = (int64_t)bytes / 16;  // n is a multiple of 256 * 4 * blocks below
+    for (int blocks : {1024, 2048, 4096, 8192, 16384}) {
+        char nm[96];
+        snprintf(nm, sizeof nm, "linear blocks=%d NT=0", blocks);
+        time_it(nm, [&] { hipLaunchKernelGGL((copy_linear<0>), dim3(blocks), dim3(256), 0, 0, in, out, n); });
+        snprintf(nm, sizeof nm, "linear blocks=%d NT=1", blocks);
+        time_it(nm, [&] { hipLaunchKernelGGL((copy_linear<1>), dim3(blocks), dim3(256), 0, 0, in, out, n); });
+        snprintf(nm, sizeof nm, "linear4 blocks=%d NT=1", blocks);
+        time_it(nm, [&] { hipLaunchKernelGGL((copy_linear_u<1, 4>), dim3(blocks), dim3(256), 0, 0, in, out, n); });
+    }
     for (int wpc : {4, 8, 16, 32}) {
         run<4, 0>(in, out, wpc, cus);
         run<4, 1>(in, out, wpc, cus);
