@@ -76,7 +76,7 @@ struct golhip_engine {
     int world_size = 1;
     int k = 1, halo = 0, band_rows = 0;
     int count_window = 4096;  // generations per count-window finalize
-    int variant = golhip::kVariantChainLdsPf;  // fastest measured (profiles/r01_tune_*)
+    int variant = golhip::kVariantDriftLds;  // fastest measured (profiles/r01_tune_*)
     int cus = 0;                 // compute units of the first device (grid sizing)
     int waves_per_cu[golhip::kMaxK + 1][golhip::kNumVariants] = {};  // occupancy cache per (K, variant)
     bool rank_mode = false;
@@ -225,6 +225,7 @@ int setup_engine(golhip_t h, int width, int height, int world, int k) {
                      : std::strcmp(e, "skewlds") == 0 ? golhip::kVariantSkewLdsPf
                      : std::strcmp(e, "skewlds2") == 0 ? golhip::kVariantSkewLdsD2
                      : std::strcmp(e, "chainlds2") == 0 ? golhip::kVariantChainLdsD2
+                     : std::strcmp(e, "driftlds") == 0 ? golhip::kVariantDriftLds
                                                      : golhip::kVariantChainLdsPf;
     return GOLHIP_OK;
 }
@@ -259,7 +260,8 @@ int64_t auto_band(golhip_t h, int64_t rows_total, int K, int64_t reserve_waves =
     // The one-generation kernel (K = 1, production variant) is HBM-bound: it runs best with 2
     // long-streaming waves per SIMD in one round (measured: 2/SIMD 21.9, 4/SIMD 21.1, 1/SIMD
     // 19.6 TCUPS at 65536^2; uneven rounds lose 10-20 %, profiles/r01_tune_step1.txt).
-    const bool step1 = K == 1 && h->variant == golhip::kVariantChainLdsPf;
+    const bool step1 = K == 1 && (h->variant == golhip::kVariantChainLdsPf ||
+                                  h->variant == golhip::kVariantDriftLds);
     const int64_t capacity = (int64_t)h->cus * (step1 ? golhip::kStep1WavesPerCu : wpc);
     constexpr int64_t kMaxBand = 4096;
     const bool skew = h->variant == golhip::kVariantSkew || h->variant == golhip::kVariantSkewD2 ||
@@ -319,7 +321,7 @@ int64_t auto_band(golhip_t h, int64_t rows_total, int K, int64_t reserve_waves =
 // when even minimal bands leave the chip short of waves (small boards, latency-bound), else 1.
 // GOLHIP_SPLIT=1/2/4 forces it (tests, tuning).
 int pick_split(golhip_t h, int64_t rows_total, int K) {
-    if (h->variant != golhip::kVariantChainLdsPf) return 1;
+    if (h->variant != golhip::kVariantChainLdsPf && h->variant != golhip::kVariantDriftLds) return 1;
     if (h->force_split > 0)
         return h->force_split > 1 && golhip::stencil_split_supported(K, h->force_split)
                    ? h->force_split

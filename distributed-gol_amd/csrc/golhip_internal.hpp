@@ -40,7 +40,8 @@ constexpr int kVariantSkewLdsPf = 4;   // input rows prefetched by LDS-DMA inste
 constexpr int kVariantChainLdsPf = 5;
 constexpr int kVariantSkewLdsD2 = 6;   // LDS-DMA ring, 2 words (64 cells) per lane
 constexpr int kVariantChainLdsD2 = 7;
-constexpr int kNumVariants = 8;
+constexpr int kVariantDriftLds = 8;    // chained LDS-DMA levels with drifting row sums (K <= 16)
+constexpr int kNumVariants = 9;
 inline int variant_words(int v) {
     return (v == kVariantSkewD2 || v == kVariantChainD2 || v == kVariantSkewLdsD2 ||
             v == kVariantChainLdsD2)
@@ -51,7 +52,8 @@ inline int variant_words(int v) {
 // words with the half-word halo (D = 1, K <= 16: lanes 0 and 63 own half a word each).
 constexpr int kStep1WavesPerCu = 8;  // gol_step1 grid: resident waves per CU it is sized for
 inline int chunk_words(int K, int variant) {
-    if (K == 1 && variant == kVariantChainLdsPf) return 256;  // gol_step1: 4 words x 64 lanes
+    if (K == 1 && (variant == kVariantChainLdsPf || variant == kVariantDriftLds))
+        return 256;  // gol_step1: 4 words x 64 lanes
     const int d = variant_words(variant);
     return (d == 1 && K <= 16) ? 63 : 62 * d;
 }

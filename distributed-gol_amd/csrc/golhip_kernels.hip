@@ -11,8 +11,10 @@
 //     The outer bits of lanes 0 and 63 go stale one bit per generation (their outer neighbour
 //     is outside the wave): for K <= 16 lane 0 still owns its upper and lane 63 its lower half
 //     word (63 words per wave), for K <= 32 lanes 0 and 63 are pure halo (62 words per wave);
-//   * horizontal neighbours cross lanes with DPP wave_shr:1 / wave_shl:1 and are merged with
-//     v_alignbit; the sums and the rule are v_bitop3 (gfx950): 13 VALU per word per generation;
+//   * horizontal neighbours cross lanes with DPP and are merged with v_alignbit; the production
+//     variant (DR) uses drifting row sums, which need only the west neighbour: one DPP + 2
+//     v_alignbit per row, the sums and the rule are v_bitop3 (gfx950): 12 VALU per word per
+//     generation (13 with the two-sided sums);
 //   * each wave streams down a band of rows keeping, per generation level, the last two rows'
 //     (sum, carry, cell) in registers: one input row in -> one row out per level per step, so a
 //     launch advances K generations while reading the board once and writing it once.
@@ -84,6 +86,27 @@ __device__ __forceinline__ void row_sum3(const Words<D> &c, Words<D> &s, Words<D
     }
 }
 
+// Drifting 3-cell sums (DR variants, D = 1): only the WEST neighbour word is needed.  Position P
+// of the result holds the sum of cells P-2, P-1, P of the input, i.e. the sum centred on cell
+// P-1, and the centre cell P-1 itself (ctr): each generation moves the row one bit east in the
+// lane's frame, so a level costs one cross-lane move instead of two.  Nothing is lost at the east
+// edge (position 63*32+31 needs nothing beyond its own lane); the west edge goes stale two bits
+// per generation instead of one bit at each edge, the same cells in total.
+template <class N = NoNb>
+__device__ __forceinline__ void row_sum3_drift(uint32_t c, uint32_t &s, uint32_t &cy,
+                                               uint32_t &ctr, const N &nb = N{}) {
+    uint32_t wl;
+    if constexpr (std::is_same_v<N, Nb>)
+        wl = nb.wl;
+    else
+        wl = lane_from_west(c);
+    const uint32_t w1 = __builtin_amdgcn_alignbit(c, wl, 31);  // cell x-1 onto x
+    const uint32_t w2 = __builtin_amdgcn_alignbit(c, wl, 30);  // cell x-2 onto x
+    s = GOL_BOP3(w2, w1, c, kXor3);
+    cy = GOL_BOP3(w2, w1, c, kMaj);
+    ctr = w1;
+}
+
 // B3/S23 from three rows' 3-cell sums: S9 = 9-cell sum including the centre cell mc;
 // alive next iff S9 == 3, or S9 == 4 and the cell is alive (server/server.go:35-52).
 // S9 = o + 2T with T = k + p + 2q (o,k: full adder of the sum bits, p,q: of the carries).
@@ -111,18 +134,24 @@ struct RowState {
 
 // One level update: `in` is the new row (below), `above`/`mid` the two previous rows of the level.
 // Writes the next generation of `mid` to nx and stores `in`'s state into `above` (now free).
-template <int D, class N = NoNb>
+// DR: drifting sums (row_sum3_drift); the state keeps the drifted centre cells.
+template <int D, bool DR = false, class N = NoNb>
 __device__ __forceinline__ void level_update(RowState<D> &above, const RowState<D> &mid,
                                              const Words<D> &in, Words<D> &nx, const N &nb = N{}) {
-    Words<D> ns, ncy;
-    row_sum3<D>(in, ns, ncy, nb);
+    Words<D> ns, ncy, nc = in;
+    if constexpr (DR) {
+        static_assert(D == 1, "drift needs one word per lane");
+        row_sum3_drift<N>(in.w[0], ns.w[0], ncy.w[0], nc.w[0], nb);
+    } else {
+        row_sum3<D>(in, ns, ncy, nb);
+    }
 #pragma unroll
     for (int d = 0; d < D; ++d)
         nx.w[d] = life_next(above.s.w[d], above.cy.w[d], mid.s.w[d], mid.cy.w[d], mid.c.w[d],
                             ns.w[d], ncy.w[d]);
     above.s = ns;
     above.cy = ncy;
-    above.c = in;
+    above.c = nc;
 }
 
 template <int D>
@@ -163,11 +192,15 @@ __device__ __forceinline__ void static_for(std::integer_sequence<int, I...>, F &
 
 // Level update without the rule: only ingests the new row's 3-cell sums into the ring (pipeline
 // fill: the level's output would be garbage, but the rows it holds are needed two steps later).
-template <int D, class N = NoNb>
+template <int D, bool DR = false, class N = NoNb>
 __device__ __forceinline__ void level_ingest(RowState<D> &above, const Words<D> &in,
                                              const N &nb = N{}) {
-    row_sum3<D>(in, above.s, above.cy, nb);
-    above.c = in;
+    if constexpr (DR) {
+        row_sum3_drift<N>(in.w[0], above.s.w[0], above.cy.w[0], above.c.w[0], nb);
+    } else {
+        row_sum3<D>(in, above.s, above.cy, nb);
+        above.c = in;
+    }
 }
 
 // Output rows [ya, yb) of band `bandi` of a launch (range 0 bands first, then range 1).
@@ -271,11 +304,16 @@ __device__ __forceinline__ void flush_counts(const uint32_t (&acc)[NL], int j0, 
 //               level j produced in the same step).
 // SKEW = true : level j consumes the row level j-1 produced in the PREVIOUS step, so the K level
 //               updates of a step are independent (K-way ILP); the pipeline is K-1 steps deeper.
-template <int K, bool COUNT, bool SKEW, int D, int PF, bool HH>
+// DR = true: drifting row sums (row_sum3_drift, one cross-lane move per level update instead of
+//             two); level j's rows sit j+1 bits east in the lane frame, the stored level-K row is
+//             shifted back by one DPP + v_alignbit per stored word, and the per-level count masks
+//             follow the drift.  Needs the half-word halo geometry (D = 1, K <= 16, chained).
+template <int K, bool COUNT, bool SKEW, int D, int PF, bool HH, bool DR = false>
 __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ in,
                                                    uint32_t *__restrict__ out, StencilParams p,
                                                    unsigned long long *__restrict__ slots) {
     static_assert(!HH || (D == 1 && K <= 16), "half-word halo needs D = 1, K <= 16");
+    static_assert(!DR || (HH && !SKEW), "drift needs the half-word halo, chained levels");
     const int lane = threadIdx.x & 63;
     // wave index made provably uniform so every band/row quantity lives in SGPRs
     const int64_t wave =
@@ -301,6 +339,11 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
         out + (int64_t)ya * p.pitch, 0, (yb - ya) * rowbytes, kBufferRsrcWord3);
     const LaneStore ls = lane_store<HH>(lane, colraw, col, p.wd);
     const uint32_t own_mask = ls.own_mask;
+    // DR: the owned mask of the lane to the west (its cells drift into this lane's low bits)
+    // (bound_ctrl: lane 0 reads 0.  No lane-select around the DPP: in a divergent branch lane 0
+    // would be off in EXEC and lane 1 would read nothing)
+    const uint32_t own_west =
+        DR ? (uint32_t)__builtin_amdgcn_mov_dpp((int)own_mask, 0x138 /* wave_shr:1 */, 0xf, 0xf, true) : 0u;
     constexpr int NSTORE = HH ? 3 : 1;  // vector-memory stores per step
     auto store_row = [&](const Words<D> &v, int rowoff) { golhip::store_row<D, HH>(orsrc, ls, v, rowoff); };
 
@@ -343,25 +386,29 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
             if (FILL && FST < 2 * j + 2) {  // folds away: FST and (unrolled) j are constants
                 if (FST >= 2 * j) {
                     if (j == 0)
-                        level_ingest<D>(PAR == 0 ? X[j] : Y[j], lin, nb0);
+                        level_ingest<D, DR>(PAR == 0 ? X[j] : Y[j], lin, nb0);
                     else
-                        level_ingest<D>(PAR == 0 ? X[j] : Y[j], lin);
+                        level_ingest<D, DR>(PAR == 0 ? X[j] : Y[j], lin);
                 }
                 if (j == K - 1) store_row(lin, kOutOfRange);  // keep the per-step store count
                 continue;
             }
             Words<D> nx;
             if (j == 0)  // level 0 takes the new row with its given neighbours (if any)
-                level_update<D>(PAR == 0 ? X[j] : Y[j], PAR == 0 ? Y[j] : X[j], lin, nx, nb0);
+                level_update<D, DR>(PAR == 0 ? X[j] : Y[j], PAR == 0 ? Y[j] : X[j], lin, nx, nb0);
             else
-                level_update<D>(PAR == 0 ? X[j] : Y[j], PAR == 0 ? Y[j] : X[j], lin, nx);
+                level_update<D, DR>(PAR == 0 ? X[j] : Y[j], PAR == 0 ? Y[j] : X[j], lin, nx);
             if (COUNT) {
                 const int r = SKEW ? st - K - 1 - 2 * j : st - K - (j + 1);
-                if (r >= 0 && r < nrows) acc[j] += __builtin_popcount(nx.w[0] & own_mask) +
+                // DR: level j's row sits j+1 bits east, and so do its owned cells
+                const uint32_t m = DR ? __builtin_amdgcn_alignbit(own_mask, own_west, 31 - j) : own_mask;
+                if (r >= 0 && r < nrows) acc[j] += __builtin_popcount(nx.w[0] & m) +
                                                    (D == 2 ? __builtin_popcount(nx.w[D - 1] & own_mask) : 0);
             }
             if (j == K - 1) {
                 const int r = st - lag;  // stored row - ya
+                if constexpr (DR)  // back to the board frame: K bits west
+                    nx.w[0] = __builtin_amdgcn_alignbit(lane_from_east(nx.w[0]), nx.w[0], K);
                 store_row(nx, (r >= 0 && r < nrows) ? r * rowbytes : kOutOfRange);
                 if (PF) asm volatile("" ::: "memory");
             } else if (SKEW) {
@@ -1018,17 +1065,17 @@ inline const void *step1_fn() {
     }
 }
 
-template <int K, bool SKEW, int D, int PF = 0>
+template <int K, bool SKEW, int D, int PF = 0, bool DR = false>
 hipError_t launch_stencil_k(const uint32_t *in, uint32_t *out, const StencilParams &p,
                             unsigned long long *slots, hipStream_t s) {
     const int64_t waves = p.nbands * (int64_t)p.nchunks;
     const unsigned blocks = (unsigned)((waves + 3) / 4);
     if (blocks == 0) return hipSuccess;
     if (slots)
-        hipLaunchKernelGGL((gol_stencil<K, true, SKEW, D, PF, kHalfHalo<K, D>>), dim3(blocks), dim3(256),
+        hipLaunchKernelGGL((gol_stencil<K, true, SKEW, D, PF, kHalfHalo<K, D>, DR>), dim3(blocks), dim3(256),
                            lds_pad_bytes(), s, in, out, p, slots);
     else
-        hipLaunchKernelGGL((gol_stencil<K, false, SKEW, D, PF, kHalfHalo<K, D>>), dim3(blocks), dim3(256),
+        hipLaunchKernelGGL((gol_stencil<K, false, SKEW, D, PF, kHalfHalo<K, D>, DR>), dim3(blocks), dim3(256),
                            lds_pad_bytes(), s, in, out, p, slots);
     return hipGetLastError();
 }
@@ -1046,6 +1093,10 @@ hipError_t launch_variant(int variant, const uint32_t *in, uint32_t *out, const 
             return launch_stencil_k<K, false, 1, 1>(in, out, p, slots, s);
         case kVariantSkewLdsD2: return launch_stencil_k<K, true, 2, 1>(in, out, p, slots, s);
         case kVariantChainLdsD2: return launch_stencil_k<K, false, 2, 1>(in, out, p, slots, s);
+        case kVariantDriftLds:
+            if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
+            else if constexpr (K > 16) return launch_stencil_k<K, false, 1, 1>(in, out, p, slots, s);
+            else return launch_stencil_k<K, false, 1, 1, true>(in, out, p, slots, s);
         default: return launch_stencil_k<K, true, 1>(in, out, p, slots, s);
     }
 }
@@ -1062,6 +1113,9 @@ const void *variant_fn(int variant) {
             return (const void *)gol_stencil<K, false, false, 1, 1, kHalfHalo<K, 1>>;
         case kVariantSkewLdsD2: return (const void *)gol_stencil<K, false, true, 2, 1, kHalfHalo<K, 2>>;
         case kVariantChainLdsD2: return (const void *)gol_stencil<K, false, false, 2, 1, kHalfHalo<K, 2>>;
+        case kVariantDriftLds:
+            if constexpr (K == 1) return step1_fn();
+            else return (const void *)gol_stencil<K, false, false, 1, 1, kHalfHalo<K, 1>, (K <= 16)>;
         default: return (const void *)gol_stencil<K, false, true, 1, 0, kHalfHalo<K, 1>>;
     }
 }

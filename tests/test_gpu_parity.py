@@ -208,7 +208,7 @@ def test_graph_replay_matches_launches(golhip, oracle, monkeypatch, k):
     assert len(cells) == int((exp == 255).sum())
 
 
-@pytest.mark.parametrize("variant", ["chainlds", "skewlds", "chainlds2", "skewlds2", "chain", "skew", "chain2", "skew2"])
+@pytest.mark.parametrize("variant", ["chainlds", "driftlds", "skewlds", "chainlds2", "skewlds2", "chain", "skew", "chain2", "skew2"])
 @pytest.mark.parametrize("k", [1, 6, 16])
 def test_every_kernel_variant(golhip, oracle, monkeypatch, variant, k):
     """Every stencil variant (chained/skewed levels, 1 or 2 words per lane, register or LDS-DMA
@@ -223,6 +223,24 @@ def test_every_kernel_variant(golhip, oracle, monkeypatch, variant, k):
             out, counts, _, _ = run_engine(golhip, board, turns, k=k, counts=True, band_rows=band)
             assert np.array_equal(out, exp), (variant, k, h, w, band)
             assert np.array_equal(counts.astype(np.int64), exp_counts), (variant, k, h, w, band)
+
+
+@pytest.mark.parametrize("k", [2, 4, 6, 8, 12, 16, 32])
+def test_drift_variant_every_k(golhip, oracle, monkeypatch, k):
+    """The drifting-sum stencil (rows move one bit east per level, one DPP per level update):
+    every launch depth, per-turn counts (per-level drifted ownership masks), multi-chunk rows
+    with a partial last chunk and widths that are not a multiple of 128 (replicated torus)."""
+    monkeypatch.setenv("GOLHIP_VARIANT", "driftlds")
+    for (h, w) in [(64, 4160), (35, 2016), (130, 8192), (9, 96)]:
+        rng = np.random.default_rng(h * 31 + w + k)
+        board = ((rng.random((h, w)) < 0.37) * 255).astype(np.uint8)
+        turns = 3 * k + 5
+        exp, exp_counts = oracle.packed_run(board, turns)
+        for band in (0, 3, 40):
+            out, counts, cells, count = run_engine(golhip, board, turns, k=k, counts=True, band_rows=band)
+            assert np.array_equal(out, exp), (k, h, w, band)
+            assert np.array_equal(counts.astype(np.int64), exp_counts), (k, h, w, band)
+            assert count == int((exp == 255).sum())
 
 
 @pytest.mark.parametrize("split", [2, 4])
