@@ -641,6 +641,7 @@ __device__ __forceinline__ void split_role(const uint32_t *__restrict__ in, uint
                                            int lane, uint32_t (*xring)[2][64],
                                            uint32_t (*ring)[64]) {
     constexpr bool HH = K <= 16;
+    constexpr bool DR = HH;                 // drifting row sums (see gol_stencil)
     constexpr int NL = K / S, J0 = R * NL;  // this wave's levels: [J0, J0 + NL)
     constexpr int PL = 8;                   // LDS-DMA ring depth (wave 0)
     constexpr int LAG = 2 * K + S - 1;
@@ -655,6 +656,8 @@ __device__ __forceinline__ void split_role(const uint32_t *__restrict__ in, uint
     const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
         out + (int64_t)ya * p.pitch, 0, (yb - ya) * rowbytes, kBufferRsrcWord3);
     const LaneStore ls = lane_store<HH>(lane, colraw, col, p.wd);
+    const uint32_t own_west =
+        DR ? (uint32_t)__builtin_amdgcn_mov_dpp((int)ls.own_mask, 0x138 /* wave_shr:1 */, 0xf, 0xf, true) : 0u;
     RowStream rows(p, ya - K);
 
     RowState<1> X[NL], Y[NL];
@@ -693,18 +696,19 @@ __device__ __forceinline__ void split_role(const uint32_t *__restrict__ in, uint
         for (int jl = 0; jl < NL; ++jl) {
             const int j = J0 + jl;
             if (FST >= 0 && FST < 2 * j + 2 + R) {  // folds away: FST and (unrolled) j constant
-                if (FST >= 2 * j + R) level_ingest<1>(PAR == 0 ? X[jl] : Y[jl], nc);
+                if (FST >= 2 * j + R) level_ingest<1, DR>(PAR == 0 ? X[jl] : Y[jl], nc);
                 nc.w[0] = 0;
                 continue;
             }
             Words<1> nx;
             if (PAR == 0)
-                level_update<1>(X[jl], Y[jl], nc, nx);
+                level_update<1, DR>(X[jl], Y[jl], nc, nx);
             else
-                level_update<1>(Y[jl], X[jl], nc, nx);
+                level_update<1, DR>(Y[jl], X[jl], nc, nx);
             if (COUNT) {
                 const int rr = st - K - (j + 1) - R;
-                if (rr >= 0 && rr < nrows) acc[jl] += __builtin_popcount(nx.w[0] & ls.own_mask);
+                const uint32_t m = DR ? __builtin_amdgcn_alignbit(ls.own_mask, own_west, 31 - j) : ls.own_mask;
+                if (rr >= 0 && rr < nrows) acc[jl] += __builtin_popcount(nx.w[0] & m);
             }
             nc = nx;
         }
@@ -712,6 +716,8 @@ __device__ __forceinline__ void split_role(const uint32_t *__restrict__ in, uint
             xring[R][st & 1][lane] = nc.w[0];
         } else {
             const int rr = st - LAG;
+            if constexpr (DR)  // back to the board frame: K bits west
+                nc.w[0] = __builtin_amdgcn_alignbit(lane_from_east(nc.w[0]), nc.w[0], K);
             store_row<1, HH>(orsrc, ls, nc, (rr >= 0 && rr < nrows) ? rr * rowbytes : kOutOfRange);
         }
         // hand-off visible to the next wave, and this step's reads done before slots are reused
