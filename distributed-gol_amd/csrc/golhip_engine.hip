@@ -225,8 +225,8 @@ int setup_engine(golhip_t h, int width, int height, int world, int k) {
                      : std::strcmp(e, "skewlds") == 0 ? golhip::kVariantSkewLdsPf
                      : std::strcmp(e, "skewlds2") == 0 ? golhip::kVariantSkewLdsD2
                      : std::strcmp(e, "chainlds2") == 0 ? golhip::kVariantChainLdsD2
-                     : std::strcmp(e, "driftlds") == 0 ? golhip::kVariantDriftLds
-                                                     : golhip::kVariantChainLdsPf;
+                     : std::strcmp(e, "chainlds") == 0 ? golhip::kVariantChainLdsPf
+                                                       : golhip::kVariantDriftLds;  // driftlds
     return GOLHIP_OK;
 }
 
@@ -291,12 +291,15 @@ int64_t auto_band(golhip_t h, int64_t rows_total, int K, int64_t reserve_waves =
         // a multiple lose 5-10 % the same way.
         const int64_t simds = 4 * (int64_t)h->cus;  // gfx9: 4 SIMDs per CU
         const int64_t m0 = std::max<int64_t>(2, 2 * (int64_t)wpc / 4);
-        const double work = (double)rows_total * (double)nchunks;
+        // The concurrent boundary bands (reserve_waves waves of K rows each) are short: they count
+        // by their rows of work, not as whole wave slots (a full slot each pushed the 65536-row
+        // interior from 264- to 272-row bands: -2.5 % on the RCCL ring of one).
+        const double work = (double)rows_total * (double)nchunks + (double)reserve_waves * K;
         // Among m within 1 % of the least cost take the largest (more, shorter bands measured
         // 3 % faster at 262144^2: band 2232 vs 3728).
         std::vector<std::pair<int64_t, double>> cand;  // (band, cost) per m
         for (int64_t m = m0; m <= 2 * m0 || cand.empty(); ++m) {
-            const double slots = (double)(m * simds - reserve_waves);
+            const double slots = (double)(m * simds);
             if (slots <= 0) continue;
             const int64_t b = aligned(std::max<int64_t>(1, (int64_t)std::ceil(work / slots)));
             if (b > kMaxBand && m < 64) continue;
