@@ -339,11 +339,12 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
         out + (int64_t)ya * p.pitch, 0, (yb - ya) * rowbytes, kBufferRsrcWord3);
     const LaneStore ls = lane_store<HH>(lane, colraw, col, p.wd);
     const uint32_t own_mask = ls.own_mask;
-    // DR: the owned mask of the lane to the west (its cells drift into this lane's low bits)
-    // (bound_ctrl: lane 0 reads 0.  No lane-select around the DPP: in a divergent branch lane 0
-    // would be off in EXEC and lane 1 would read nothing)
-    const uint32_t own_west =
-        DR ? (uint32_t)__builtin_amdgcn_mov_dpp((int)own_mask, 0x138 /* wave_shr:1 */, 0xf, 0xf, true) : 0u;
+    // DR counts need no per-level mask: level j's row sits d = j+1 bits east, so positions
+    // [32, 2048) (lanes 1..63 in full) hold cells [2016c - d, 2016(c+1) - d) of chunk c -- windows
+    // that tile the row at every level (valid: the drift leaves [2d, 2048) valid, 2d <= 32) -- and
+    // the last chunk's window ends at the row end (colraw < wd) for every d.  So every lane counts
+    // its whole word and the lanes outside the window drop their sums once, at the flush.
+    const bool count_lane = lane >= 1 && colraw < p.wd;
     constexpr int NSTORE = HH ? 3 : 1;  // vector-memory stores per step
     auto store_row = [&](const Words<D> &v, int rowoff) { golhip::store_row<D, HH>(orsrc, ls, v, rowoff); };
 
@@ -400,8 +401,7 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
                 level_update<D, DR>(PAR == 0 ? X[j] : Y[j], PAR == 0 ? Y[j] : X[j], lin, nx);
             if (COUNT) {
                 const int r = SKEW ? st - K - 1 - 2 * j : st - K - (j + 1);
-                // DR: level j's row sits j+1 bits east, and so do its owned cells
-                const uint32_t m = DR ? __builtin_amdgcn_alignbit(own_mask, own_west, 31 - j) : own_mask;
+                const uint32_t m = DR ? ~0u : own_mask;  // DR: whole words, see count_lane
                 if (r >= 0 && r < nrows) acc[j] += __builtin_popcount(nx.w[0] & m) +
                                                    (D == 2 ? __builtin_popcount(nx.w[D - 1] & own_mask) : 0);
             }
@@ -521,7 +521,13 @@ __global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
 
-    if (COUNT) flush_counts<K>(acc, 0, lane, wave, slots);
+    if (COUNT) {
+        if (DR && !count_lane) {
+#pragma unroll
+            for (int j = 0; j < K; ++j) acc[j] = 0;
+        }
+        flush_counts<K>(acc, 0, lane, wave, slots);
+    }
 }
 
 // ---------------------------------------------------------------- one generation (K = 1)
@@ -656,8 +662,7 @@ __device__ __forceinline__ void split_role(const uint32_t *__restrict__ in, uint
     const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
         out + (int64_t)ya * p.pitch, 0, (yb - ya) * rowbytes, kBufferRsrcWord3);
     const LaneStore ls = lane_store<HH>(lane, colraw, col, p.wd);
-    const uint32_t own_west =
-        DR ? (uint32_t)__builtin_amdgcn_mov_dpp((int)ls.own_mask, 0x138 /* wave_shr:1 */, 0xf, 0xf, true) : 0u;
+    const bool count_lane = lane >= 1 && colraw < p.wd;  // DR count window (see gol_stencil)
     RowStream rows(p, ya - K);
 
     RowState<1> X[NL], Y[NL];
@@ -707,7 +712,7 @@ __device__ __forceinline__ void split_role(const uint32_t *__restrict__ in, uint
                 level_update<1, DR>(Y[jl], X[jl], nc, nx);
             if (COUNT) {
                 const int rr = st - K - (j + 1) - R;
-                const uint32_t m = DR ? __builtin_amdgcn_alignbit(ls.own_mask, own_west, 31 - j) : ls.own_mask;
+                const uint32_t m = DR ? ~0u : ls.own_mask;
                 if (rr >= 0 && rr < nrows) acc[jl] += __builtin_popcount(nx.w[0] & m);
             }
             nc = nx;
@@ -742,7 +747,13 @@ __device__ __forceinline__ void split_role(const uint32_t *__restrict__ in, uint
         }
     }
     if (R == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the ring
-    if (COUNT) flush_counts<NL>(acc, J0, lane, group, slots);
+    if (COUNT) {
+        if (DR && !count_lane) {
+#pragma unroll
+            for (int j = 0; j < NL; ++j) acc[j] = 0;
+        }
+        flush_counts<NL>(acc, J0, lane, group, slots);
+    }
 }
 
 template <int K, bool COUNT, int S>
