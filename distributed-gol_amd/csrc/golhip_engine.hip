@@ -320,9 +320,9 @@ int64_t auto_band(golhip_t h, int64_t rows_total, int K, int64_t reserve_waves =
     return std::min(band, std::max<int64_t>(rows_total, 1));
 }
 
-// Waves per (band, chunk) of a launch over rows_total rows: the level-split kernel (S = 2 or 4)
+// Waves per (band, chunk) of a launch over rows_total rows: the level-split kernel (S = 2, 4 or 8)
 // when even minimal bands leave the chip short of waves (small boards, latency-bound), else 1.
-// GOLHIP_SPLIT=1/2/4 forces it (tests, tuning).
+// GOLHIP_SPLIT=1/2/4/8 forces it (tests, tuning).
 int pick_split(golhip_t h, int64_t rows_total, int K) {
     if (h->variant != golhip::kVariantChainLdsPf && h->variant != golhip::kVariantDriftLds) return 1;
     if (h->force_split > 0)
@@ -339,6 +339,10 @@ int pick_split(golhip_t h, int64_t rows_total, int K) {
     int &wpc = h->waves_per_cu[K][h->variant];
     if (wpc == 0) wpc = golhip::stencil_waves_per_cu(K, h->variant);
     const int64_t capacity = (int64_t)h->cus * wpc;
+    // S = 8 (two levels per wave at K = 16) on the boards that fit S = 4 in one round: its waves
+    // are light (few VGPRs), so up to two rounds' worth: 5120^2 with counts 1.70 -> 1.58 us per
+    // turn, 4096^2 1.49 -> 1.35 (profiles/r01_tune_small_split8.txt)
+    if (golhip::stencil_split_supported(K, 8) && waves1 * 8 <= 2 * capacity) return 8;
     for (int S : {4, 2})
         if (golhip::stencil_split_supported(K, S) && waves1 * S <= capacity) return S;
     return 1;

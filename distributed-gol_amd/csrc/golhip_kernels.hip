@@ -1156,6 +1156,7 @@ hipError_t launch_split_ks(const uint32_t *in, uint32_t *out, const StencilParam
 bool stencil_split_supported(int K, int S) {
     if (S == 2) return K == 4 || K == 6 || K == 8 || K == 12 || K == 16 || K == 32;
     if (S == 4) return K == 4 || K == 8 || K == 12 || K == 16 || K == 32;
+    if (S == 8) return K == 8 || K == 16 || K == 32;
     return false;
 }
 
@@ -1167,6 +1168,7 @@ hipError_t launch_stencil_split(int K, int S, const uint32_t *in_row0, uint32_t 
     GOL_SPLIT_CASE(16, 2) GOL_SPLIT_CASE(32, 2)
     GOL_SPLIT_CASE(4, 4) GOL_SPLIT_CASE(8, 4) GOL_SPLIT_CASE(12, 4) GOL_SPLIT_CASE(16, 4)
     GOL_SPLIT_CASE(32, 4)
+    GOL_SPLIT_CASE(8, 8) GOL_SPLIT_CASE(16, 8) GOL_SPLIT_CASE(32, 8)
 #undef GOL_SPLIT_CASE
     return hipErrorInvalidValue;
 }

@@ -243,7 +243,7 @@ def test_drift_variant_every_k(golhip, oracle, monkeypatch, k):
             assert count == int((exp == 255).sum())
 
 
-@pytest.mark.parametrize("split", [2, 4])
+@pytest.mark.parametrize("split", [2, 4, 8])
 @pytest.mark.parametrize("k", [4, 6, 8, 16, 32])
 def test_level_split_kernel(golhip, oracle, monkeypatch, split, k):
     """The level-split stencil (gol_stencil_split: the K levels of a band over S waves of one
