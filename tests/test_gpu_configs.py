@@ -76,3 +76,68 @@ def test_cfg4_262144_window_locality(golhip, oracle, strips):
             assert np.array_equal(got[t:-t], win[t:-t]), y0
         assert e.alive_count() == int(counts[-1])
 
+
+def test_cfg5_host_run_ticker_and_keys(golhip, oracle, tmp_path):
+    """configs[4] through the C++ host (`gol::Run`, the gol.Run mirror): 1e6 turns with the 2 s
+    AliveCellsCount ticker and timed keypresses p (pause, held 2.5 s so the ticker fires while
+    paused), s (snapshot while paused), p (resume).  Every tick's count must be the count after its
+    reported turn (gol/distributor.go:168-191), the snapshot must be the board after its turn
+    (:93-103,118-119), and the final alive list / PGM the board after 1e6 turns (:235-253)."""
+    import re
+    import subprocess
+    import time
+
+    from conftest import ROOT
+
+    gol = ROOT / "distributed-gol_amd" / "lib" / "gol"
+    assert gol.exists(), "host binary missing: run __graft_entry__.build()"
+    b = np.zeros((4096, 4096), dtype=np.uint8)
+    golhip.place(b, golhip.parse_rle((GOLDEN / "gosper_gun.rle").read_text()), 64, 64)
+    golhip.place(b, golhip.parse_rle((GOLDEN / "r_pentomino.rle").read_text()), 2048, 2048)
+    turns = 1000000
+    with golhip.Engine(4096, 4096, k=16) as e:
+        e.load(b)
+        counts = [int(c) for c in e.step(turns, counts=True)]
+    initial = int((b == 255).sum())
+
+    def count_after(t):
+        return initial if t == 0 else counts[t - 1]
+
+    (tmp_path / "images").mkdir()
+    (tmp_path / "images" / "4096x4096.pgm").write_bytes(oracle.pgm_bytes(b))
+    out = tmp_path / "out"
+    p = subprocess.Popen([str(gol), "-w", "4096", "-h", "4096", "-turns", str(turns), "-k", "16",
+                          "-images", str(tmp_path / "images"), "-out", str(out)],
+                         stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+    time.sleep(0.8)
+    p.stdin.write("p\n")
+    p.stdin.flush()
+    time.sleep(2.5)
+    p.stdin.write("s\n")
+    p.stdin.flush()
+    time.sleep(0.3)
+    p.stdin.write("p\n")
+    p.stdin.flush()
+    stdout, _ = p.communicate(timeout=90)  # closes stdin: the key reader sees EOF
+    assert p.returncode == 0, stdout[-2000:]
+    lines = [re.match(r"Completed Turns (\d+)\s+(.*)$", ln) for ln in stdout.splitlines()]
+    events = [(int(m.group(1)), m.group(2)) for m in lines if m]
+    ticks = [(t, int(s.split()[-1])) for t, s in events if s.startswith("Alive Cells")]
+    assert ticks, stdout[-2000:]
+    for t, c in ticks:
+        assert c == count_after(t), (t, c)
+    states = [s for _, s in events]
+    assert "Paused" in states and "Executing" in states, states
+    snaps = [s.split()[1] for _, s in events if s.startswith("File ") and s.split()[1] != "4096x4096x%d" % turns]
+    assert len(snaps) == 1, states
+    t_snap = int(snaps[0].rsplit("x", 1)[1])
+    _, _, snap = oracle.read_pgm(out / (snaps[0] + ".pgm"))
+    with golhip.Engine(4096, 4096, k=16) as e:
+        e.load(b)
+        e.step(t_snap)
+        assert np.array_equal(snap, e.store()), t_snap
+    assert events[-1] == (turns, "Quitting"), events[-3:]
+    final = re.search(r"Final turn (\d+): (\d+) alive cells", stdout)
+    assert final and int(final.group(1)) == turns and int(final.group(2)) == counts[-1]
+    _, _, last = oracle.read_pgm(out / ("4096x4096x%d.pgm" % turns))
+    assert int((last == 255).sum()) == counts[-1]
