@@ -96,17 +96,37 @@ for k in (16, 32):
         cfg5[f"step_k{k}"] = {"s": round(dt, 3), "us_per_turn": round(dt, 3),
                               "gcups": round(4096 * 4096 * 1e6 / dt / 1e9, 1),
                               "count_1e6": int(counts[-1])}
-with tempfile.TemporaryDirectory() as d:
-    (Path(d) / "images").mkdir()
-    (Path(d) / "images" / "4096x4096.pgm").write_bytes(oracle.pgm_bytes(b))
-    t = time.perf_counter()
-    p = subprocess.run([str(ROOT / "distributed-gol_amd/lib/gol"), "-w", "4096", "-h", "4096",
-                        "-turns", "1000000", "-k", "16", "-images", f"{d}/images", "-out", f"{d}/out"],
-                       input="", capture_output=True, text=True, timeout=600)
-    wall = time.perf_counter() - t
-    ticks = [ln for ln in p.stdout.splitlines() if "Alive Cells" in ln]
-    cfg5["host_run"] = {"wall_s": round(wall, 2), "rc": p.returncode, "ticks": len(ticks),
-                        "first_ticks": ticks[:3], "final": p.stdout.splitlines()[-1:],
-                        "note": "gol::Run with TurnComplete per turn + 2 s AliveCellsCount ticker"}
+with golhip.Engine(4096, 4096, k=16) as e:
+    e.load(b)
+    counts5 = [int(c) for c in e.step(1000000, counts=True)]
+init5 = int((b == 255).sum())
+for keys in (False, True):
+    with tempfile.TemporaryDirectory() as d:
+        (Path(d) / "images").mkdir()
+        (Path(d) / "images" / "4096x4096.pgm").write_bytes(oracle.pgm_bytes(b))
+        t = time.perf_counter()
+        p = subprocess.Popen([str(ROOT / "distributed-gol_amd/lib/gol"), "-w", "4096", "-h", "4096",
+                              "-turns", "1000000", "-k", "16", "-images", f"{d}/images",
+                              "-out", f"{d}/out"], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                             text=True)
+        if keys:  # p (hold 2.5 s: the 2 s ticker fires while paused), s, p
+            for key, wait in (("p", 0.8), ("s", 2.5), ("p", 0.3)):
+                time.sleep(wait)
+                p.stdin.write(key + "\n")
+                p.stdin.flush()
+        out, _ = p.communicate(timeout=600)
+        wall = time.perf_counter() - t
+    ticks = [ln for ln in out.splitlines() if "Alive Cells" in ln]
+    tick_ok = all(int(ln.split()[-1]) == (init5 if int(ln.split()[2]) == 0
+                                          else counts5[int(ln.split()[2]) - 1]) for ln in ticks)
+    cfg5["host_run_keys" if keys else "host_run"] = {
+        "wall_s": round(wall, 2), "rc": p.returncode, "ticks": len(ticks),
+        "ticks_match_counts": tick_ok, "first_ticks": ticks[:3],
+        "states": [ln for ln in out.splitlines() if ln.endswith(("Paused", "Executing"))
+                   or "output complete" in ln],
+        "final": out.splitlines()[-1:],
+        "note": ("gol::Run with TurnComplete per turn + 2 s AliveCellsCount ticker"
+                 + (", keys p (2.5 s) s p; wall includes the pause" if keys else
+                    "; finishes before the first 2 s tick"))}
 res["cfg5"] = cfg5
 print(json.dumps(res))
