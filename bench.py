@@ -11,12 +11,22 @@ k-row RCCL halo exchange over xGMI (weak scaling: per-GPU work fixed).  --size/-
 other boards (e.g. --size 262144 for configs[3], strong scaling).
 
 Prints ONE JSON line on rank 0 (keys per the driver contract), plus:
-  roofline     : algorithmic bytes (0.25 B per cell-update) per stencil launch / the launch's
-                 average duration from HIP events recorded on the engine's compute stream;
-  valu_roofline: the stencil's actual bound for k >= 4 -- algorithmic wave64 VALU instructions
-                 (13 per 32-cell word per generation) per second vs the issue peak of that mix;
+  roofline     : the bound of the timed kernel.  k >= 2 (temporal blocking, VALU-bound):
+                 algorithmic wave64 VALU instructions (12 per 32-cell word per generation) per
+                 launch / the launch's average duration from HIP events on the engine's compute
+                 stream, against the VALU issue peak (1024 SIMDs x 2.4 GHz / 2 cycles per wave64
+                 instruction, MI355X_MICROARCH.md "Wave scheduling"); the PMC-measured issued
+                 count (SQ_INSTS_VALU) and clock (GRBM_GUI_ACTIVE / 8 / duration) of the same
+                 kernel from profiles/pmc_traffic.json beside it.  k == 1: HBM bytes (0.25 B per
+                 cell-update) against 8 TB/s;
+  hbm_roofline : the algorithmic-HBM figure of the same timed launches (exceeds 1 for k > 1:
+                 temporal blocking reads and writes the board once per k generations);
+  parity       : alive cells after warmup + steps generations == the oracle's golden count
+                 (tests/golden/cfg3_65536_seed3_counts.csv) when that turn is pinned;
   cpu_baseline : the reference algorithm (oracle/ port of server/server.go + broker split,
-                 byte per cell, 4 servers x T threads) timed on this host on a bounded sample;
+                 byte per cell, 4 servers x 4 threads, full-world fan-out copy per server per
+                 turn, per-turn alive scan) timed on this host on a bounded sample of the same
+                 65536^2 board, plus configs[0] (512^2 x 100 turns) in full;
   k_sweep      : GCUPS per temporal-blocking depth k (N == 1 only);
   hbm_roofline_k1: the k = 1 kernel (gol_step1, no temporal reuse) against the HBM peak;
   strong_262144: configs[3] -- the 262144^2 board (seed 4) split over the N ranks, GCUPS and
@@ -41,15 +51,17 @@ import golhip  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 BYTES_PER_CELL_UPDATE = 0.25  # 1 packed bit read + 1 packed bit written per cell per generation
-# VALU roofline of the stencil (the bound for k >= 4): 12 wave64 VALU
-# instructions per 32-cell word per generation with drifting row sums (9 v_bitop3 at full rate,
-# 2 v_alignbit + 1 DPP move at half rate).  Peak issue = 1024 SIMDs x 2.4 GHz / cycles per
-# instruction, where a full-rate wave64 op takes 2 cycles (SIMD-32) and a half-rate one 4: the
-# mix averages 30 cycles per 12 instructions.  Reported as instruction issue rate (wave64 VALU
-# instructions per second).
+# VALU roofline of the stencil (the bound for k >= 2): 12 wave64 VALU
+# instructions per 32-cell word per generation with drifting row sums (9 v_bitop3, 2 v_alignbit,
+# 1 DPP move).  Peak issue = 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction
+# (SIMD-32, MI355X_MICROARCH.md "Wave scheduling"): 1.2288 T wave64-instructions/s.  The half-rate
+# ops (v_alignbit, DPP: 4 cycles, profiles/r01_ubench_valu2_clocked.txt) cap this mix at 24/30 of
+# that peak ("mix_peak").
 VALU_PER_WORD_GEN = 12
 VALU_CYCLES_PER_WORD_GEN = 9 * 2 + 3 * 4
-SIMDS, PEAK_CLOCK_GHZ = 1024, 2.4
+SIMDS, PEAK_CLOCK_GHZ, CYCLES_PER_WAVE_INSTR = 1024, 2.4, 2
+VALU_PEAK_T = SIMDS * PEAK_CLOCK_GHZ * 1e9 / CYCLES_PER_WAVE_INSTR / 1e12
+GOLDEN = ROOT / "tests" / "golden"
 
 
 def parse():
@@ -65,8 +77,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-sweep", action="store_true", help="skip the k sweep")
-    ap.add_argument("--cpu-size", type=int, default=16384)
-    ap.add_argument("--cpu-turns", type=int, default=96)
+    ap.add_argument("--cpu-size", type=int, default=65536, help="CPU baseline board (the bench board)")
+    ap.add_argument("--cpu-turns", type=int, default=2, help="CPU baseline turns (~15 s of CPU work)")
     ap.add_argument("--no-timing", action="store_true",
                     help="no per-launch HIP events in the timed region (roofline from wall time)")
     ap.add_argument("--pmc-file", default=str(ROOT / "profiles" / "pmc_traffic.json"))
@@ -96,29 +108,89 @@ def timed_steps(eng: golhip.Engine, steps: int, world: int) -> float:
     return dt
 
 
+def host_cpu() -> tuple[int, str]:
+    """Logical CPUs of this host and its CPU model (lscpu's "Model name", from /proc/cpuinfo)."""
+    model = "unknown"
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return os.cpu_count() or 0, model
+
+
 def cpu_baseline(size: int, turns: int, threads_per_server: int) -> dict:
-    """The reference's algorithm (oracle/gol_oracle.c oracle_ref_*), timed on this host."""
+    """The reference's algorithm (oracle/gol_oracle.c oracle_ref_*), timed on this host.
+
+    Sample: `turns` turns of the bench board itself (65536^2 random, seed 3) with the reference's
+    cost structure -- byte cells, branchy torus wrap + /255, fresh rows per turn, 4 broker strips
+    x `threads_per_server` goroutine-threads, a private full-world copy per server per turn (the
+    gob fan-out of broker/broker.go:51,64) and the controller's per-turn alive scan
+    (gol/distributor.go:186).  The RPC transport itself (gob encode/TCP) is not timed.  Plus
+    configs[0] in full: images/512x512.pgm for 100 turns, checked byte-exact against the
+    reference's check/images/512x512x100.pgm."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import numpy as np
 
     import oracle
 
+    nproc, model = host_cpu()
+    threads = 4 * threads_per_server
+    # configs[0] in full
+    ref = GOLDEN / "reference"
+    _, _, b512 = oracle.read_pgm(ref / "images" / "512x512.pgm")
+    t0 = time.perf_counter()
+    out512, _ = oracle.ref_run(b512, 100, threads=threads_per_server, servers=4, fanout_copy=True)
+    dt512 = time.perf_counter() - t0
+    exact = oracle.pgm_bytes(out512) == (ref / "check" / "images" / "512x512x100.pgm").read_bytes()
+
     board = oracle.unpack(oracle.init_random(size, size, seed=3), size)
     t0 = time.perf_counter()
-    oracle.ref_run(board, turns, threads=threads_per_server, servers=4, fanout_copy=False)
+    oracle.ref_run(board, turns, threads=threads_per_server, servers=4, fanout_copy=True)
     dt = time.perf_counter() - t0
     cups = size * size * turns / dt
     del board, np
     return {
         "value": round(cups / 1e9, 4),
         "unit": "GCUPS",
-        "cores": 4 * threads_per_server,
+        "cores": threads,
+        "host_cores": nproc,
+        "cpu_model": model,
+        "fanout_copy": True,
         "kind": "port",
-        "sample": (f"{size}x{size} random p=0.5 seed 3, {turns} turns of the reference algorithm "
-                   f"(byte cells, branchy torus wrap + /255, fresh rows per turn, 4 broker strips x "
-                   f"{threads_per_server} goroutine-threads = {4 * threads_per_server} OS threads); "
-                   f"gob/TCP fan-out excluded; {dt:.1f} s"),
+        "sample": (f"{size}x{size} random p=0.5 seed 3 (the bench board), {turns} turns of the "
+                   f"reference algorithm: byte cells, branchy torus wrap + /255, fresh rows per "
+                   f"turn, 4 broker strips x {threads_per_server} goroutine-threads = {threads} OS "
+                   f"threads, full-world copy per server per turn, per-turn alive scan; gob/TCP "
+                   f"transport not timed; {dt:.1f} s"),
+        "cfg1_512x100": {"s": round(dt512, 4), "gcups": round(512 * 512 * 100 / dt512 / 1e9, 4),
+                         "bit_exact_vs_reference_fixture": bool(exact)},
     }
+
+
+def golden_count(turn: int) -> int | None:
+    """The oracle's alive count of configs[2] (65536^2, seed 3) after `turn` turns, if pinned."""
+    path = GOLDEN / "cfg3_65536_seed3_counts.csv"
+    if turn < 1 or not path.exists():
+        return None
+    for line in path.read_text().splitlines()[1:]:
+        t, c = line.split(",")
+        if int(t) == turn:
+            return int(c)
+    return None
+
+
+def golden_count_cfg4(turn: int) -> int | None:
+    path = GOLDEN / "cfg4_262144_seed4_counts.csv"
+    if turn < 1 or not path.exists():
+        return None
+    for line in path.read_text().splitlines()[1:]:
+        t, c = line.split(",")
+        if int(t) == turn:
+            return int(c)
+    return None
 
 
 def main():
@@ -167,35 +239,63 @@ def main():
     gcups = total_updates / dt / 1e9
     ms_per_step = dt * 1e3 / a.steps
 
-    # roofline of the dominant kernel (gol_stencil<k>) on this rank
+    # roofline of the timed kernel (gol_stencil<k>, or gol_step1 at k = 1) on this rank, from the
+    # HIP events around the timed launches on the engine's compute stream
     avg_launch_ms = kern_ms / max(launches, 1)
     gens_per_launch = gens / max(launches, 1)
     alg_bytes_per_launch = BYTES_PER_CELL_UPDATE * local_cells * gens_per_launch
-    achieved = alg_bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
-    # VALU roofline: algorithmic wave-instructions per launch (the cells it updates, no halo or
-    # pipeline-fill work) over the launch time, against the issue peak for the same mix
+    hbm_achieved = alg_bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
+    # algorithmic wave64 VALU instructions per launch: 12 per 32-cell word per generation over the
+    # cells the launch updates (no band-halo trapezoid, pipeline fill, loop or store work)
     words_per_launch = local_cells / 32 * gens_per_launch
-    valu_instr = words_per_launch / 64 * VALU_PER_WORD_GEN
-    valu_achieved = valu_instr / (avg_launch_ms * 1e-3) / 1e12
-    valu_peak = SIMDS * PEAK_CLOCK_GHZ * 1e9 / (VALU_CYCLES_PER_WORD_GEN / VALU_PER_WORD_GEN) / 1e12
-    valu = {"bound": "valu", "achieved": round(valu_achieved, 4), "peak": round(valu_peak, 4),
-            "unit": "T wave64-instr/s", "frac": round(valu_achieved / valu_peak, 4),
-            "mix": "12 per 32-cell word per generation: 9 v_bitop3 (2 cyc) + 2 v_alignbit + 1 DPP (4 cyc)",
-            "note": "peak at 2.4 GHz; the dense start runs at 1.9-2.2 GHz (power)"}
-    traffic = None
+    valu_alg = words_per_launch / 64 * VALU_PER_WORD_GEN
+    valu_achieved = valu_alg / (avg_launch_ms * 1e-3) / 1e12
+    pmc_entry = {}
     try:
         pmc = json.loads(Path(a.pmc_file).read_text())
-        key = f"{width}x{eng.info.rows}_k{a.k}"
-        if key in pmc:
-            traffic = pmc[key]["hbm_bytes_per_launch"]
+        pmc_entry = pmc.get(f"{width}x{eng.info.rows}_k{a.k}", {})
     except Exception:
         pass
+    traffic = pmc_entry.get("hbm_bytes_per_launch")
+    uniform = launches > 0 and gens == launches * a.k  # every timed launch ran k generations
+    issued = pmc_entry.get("valu_instr_per_launch")
+    kernel_name = "gol_step1" if a.k == 1 else f"gol_stencil<{a.k}>"
+    if a.k == 1:
+        roof = {"bound": "hbm", "achieved": round(hbm_achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(hbm_achieved / HBM_PEAK_GBS, 4), "traffic": traffic}
+    else:
+        roof = {"bound": "valu", "achieved": round(valu_achieved, 4), "peak": round(VALU_PEAK_T, 4),
+                "unit": "T wave64-VALU-instr/s", "frac": round(valu_achieved / VALU_PEAK_T, 4),
+                "traffic": traffic,
+                "mix": "12 per 32-cell word per generation: 9 v_bitop3 (2 cyc) + 2 v_alignbit "
+                       "+ 1 DPP move (4 cyc): mix_peak = 24/30 of peak",
+                "mix_peak": round(VALU_PEAK_T * 24 / VALU_CYCLES_PER_WORD_GEN, 4)}
+        if issued and uniform:
+            roof["issued_pmc"] = round(issued / (avg_launch_ms * 1e-3) / 1e12, 4)
+            roof["issued_frac"] = round(issued / (avg_launch_ms * 1e-3) / 1e12 / VALU_PEAK_T, 4)
+            roof["issued_per_launch_pmc"] = issued
+        if pmc_entry.get("clock_ghz"):
+            roof["clock_ghz_pmc"] = pmc_entry["clock_ghz"]
+    roof.update({"kernel": kernel_name, "avg_launch_us": round(avg_launch_ms * 1e3, 2),
+                 "launches": launches, "gens_per_launch": round(gens_per_launch, 3)})
+    hbm_roof = {"achieved": round(hbm_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "algorithmic_over_peak": round(hbm_achieved / HBM_PEAK_GBS, 4),
+                "measured_traffic_per_launch": traffic,
+                "note": "0.25 B per cell-update; temporal blocking moves the board once per "
+                        "launch, so this exceeds 1 for k > 1 and is not the binding bound"}
+    # parity: the canary against the oracle's golden count (configs[2] board, N == 1 only)
+    parity = None
+    if world == 1 and width == 65536 and height == 65536 and a.seed == 3:
+        exp = golden_count(a.warmup + a.steps)
+        if exp is not None:
+            parity = {"turn": a.warmup + a.steps, "alive": int(alive_timed), "golden": exp,
+                      "ok": int(alive_timed) == exp}
 
     sweep = None
     k1_launch_us = None
     if world == 1 and not a.no_sweep:
         sweep = {}
-        for kk in (1, 2, 4, 8, 16, 32):
+        for kk in (1, 2, 4, 8, 12, 16, 32):
             eng.set_k(kk)
             # the first ~250 one-generation launches of a process run ~10 % slower (measured,
             # scripts/diag_k1.py), so k = 1 gets a longer untimed warmup
@@ -237,6 +337,10 @@ def main():
                   "rows_per_gpu": -(-n // world), "gcups": round(g, 1),
                   "gcups_per_gpu": round(g / world, 1), "ms_per_step": round(t * 1e3 / a.strong_steps, 4),
                   "alive_after": int(strong_alive)}
+        exp = golden_count_cfg4(a.k + a.strong_steps) if n == 262144 else None
+        if exp is not None:
+            strong["parity"] = {"turn": a.k + a.strong_steps, "golden": exp,
+                                "ok": int(strong_alive) == exp}
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
@@ -261,18 +365,9 @@ def main():
                              f"{world} row strip(s) of {local_rows} rows, k={a.k} gens/launch"),
                 "width": width, "height": height, "k": a.k, "parallelism": f"rows{world}",
             },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "kernel": "gol_step1" if a.k == 1 else f"gol_stencil<{a.k}>",
-                "avg_launch_us": round(avg_launch_ms * 1e3, 2),
-                "gens_per_launch": gens_per_launch,
-            },
-            "valu_roofline": valu,
+            "parity": parity,
+            "roofline": roof,
+            "hbm_roofline": hbm_roof,
             "cpu_baseline": cpu,
             "k_sweep_gcups": sweep,
             # the north star's HBM figure for the one-generation kernel (no temporal reuse):
@@ -291,6 +386,10 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    # a wrong board is not a result: the line above is printed for the record, then the run fails
+    bad = (parity and not parity["ok"]) or (strong and strong.get("parity") and not strong["parity"]["ok"])
+    if bad:
+        raise SystemExit("bench parity FAILED: alive count differs from the oracle's golden count")
 
 
 if __name__ == "__main__":

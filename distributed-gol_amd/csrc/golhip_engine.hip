@@ -241,6 +241,47 @@ int pick_k(int n) {
     return kk;
 }
 
+// Measured throughput of a K-generation launch, T cell-updates/s at 65536^2 (k sweep of
+// profiles/r01_bench.json: 1 -> 21.8, 2 -> 30.0, 4 -> 59.8, 32 -> 92.5; drift kernel at 8/12/16
+// from profiles/r01_tune_drift.txt; 6 interpolated), and the fixed cost of one launch (kernel
+// boundary + the last round's drain, us).
+double launch_rate_tcups(int K) {
+    switch (K) {
+        case 1: return 21.8;
+        case 2: return 30.0;
+        case 4: return 59.8;
+        case 6: return 85.0;
+        case 8: return 109.4;
+        case 12: return 116.2;
+        case 16: return 118.9;
+        case 32: return 92.5;
+        default: return 50.0;
+    }
+}
+constexpr double kLaunchOverheadUs = 4.0;
+
+// Launch depths for `n` remaining generations (n < 2 * kmax): the sequence of supported depths
+// <= kmax summing to n with the least modelled time sum(cells * K / rate(K) + overhead).  The
+// greedy largest-first split ran 20 turns as 16 + 4 (the 4-level launch at half the rate);
+// this gives 12 + 8.  The first depth of the plan is returned; callers re-plan each launch.
+int plan_first_k(int64_t n, int kmax, double cells) {
+    if (n <= 0) return 1;
+    const int N = (int)n;
+    std::vector<double> best(N + 1, 1e300);
+    std::vector<int> first(N + 1, 1);
+    best[0] = 0.0;
+    for (int m = 1; m <= N; ++m)
+        for (int K : {32, 16, 12, 8, 6, 4, 2, 1}) {
+            if (K > m || K > kmax || !golhip::stencil_k_supported(K)) continue;
+            const double c = best[m - K] + cells * K / (launch_rate_tcups(K) * 1e6) + kLaunchOverheadUs;
+            if (c < best[m]) {
+                best[m] = c;
+                first[m] = K;
+            }
+        }
+    return first[N];
+}
+
 // Rows per wave band of a stencil launch over rows_total rows.  reserve_waves: resident wave
 // slots to leave free for a concurrent launch (the boundary bands of a split board).
 int64_t auto_band(golhip_t h, int64_t rows_total, int K, int64_t reserve_waves = 0) {
@@ -348,6 +389,15 @@ int pick_split(golhip_t h, int64_t rows_total, int K) {
     return 1;
 }
 
+// Largest band the kernels' 32-bit store offsets can address: a band's output descriptor spans
+// band * rowbytes bytes, and dropped stores use offset kOutOfRange (2^30) + row * rowbytes, so
+// band * rowbytes must stay below 2^30 (golhip_kernels.hip, buffer_store_words).  At 262144 wide
+// that is 32767 rows; only --band-rows / very wide boards can reach it.
+int64_t max_band_rows(golhip_t h) {
+    const int64_t rowbytes = h->pitch * 4;
+    return std::max<int64_t>(1, ((int64_t)1 << 30) / rowbytes - 1);
+}
+
 // Launch the K-generation stencil described by p (level-split kernel when pick_split says so).
 hipError_t launch_auto(golhip_t h, int K, const uint32_t *in, uint32_t *out,
                        const StencilParams &p, unsigned long long *slots, hipStream_t s) {
@@ -365,7 +415,7 @@ StencilParams make_params(golhip_t h, const Shard &s, int K, int64_t r0b, int64_
     p.r1b = r1b;
     p.r1e = r1e;
     const int64_t total = (r0e - r0b) + (r1e - r1b);
-    p.band = auto_band(h, std::max<int64_t>(total, 1), K, reserve_waves);
+    p.band = std::min(auto_band(h, std::max<int64_t>(total, 1), K, reserve_waves), max_band_rows(h));
     p.nbands0 = (r0e - r0b + p.band - 1) / p.band;
     p.nbands = p.nbands0 + (r1e - r1b + p.band - 1) / p.band;
     p.wrap_rows = h->split ? 0 : h->height;
@@ -1032,7 +1082,9 @@ int golhip_step(golhip_t h, int64_t turns, uint64_t *alive_per_turn) {
             }
             continue;
         }
-        const int K = pick_k((int)std::min<int64_t>(left, h->k));
+        const int K = left >= 2 * (int64_t)Kfull
+                          ? Kfull
+                          : plan_first_k(left, Kfull, (double)h->L * (double)h->height);
         if (counting && win + K > h->count_window) {
             int rc = flush_counts_window(h, (int)win, done - win);
             if (rc) return rc;

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 namespace golhip {
 
 // Device layout of one row strip (see DESIGN.md "Data layout in HBM"):
@@ -56,6 +58,23 @@ inline int chunk_words(int K, int variant) {
         return 256;  // gol_step1: 4 words x 64 lanes
     const int d = variant_words(variant);
     return (d == 1 && K <= 16) ? 63 : 62 * d;
+}
+
+// Launch depths with a stencil instantiation, one translation unit each (stencil_k<K>.hip).
+#define GOLHIP_STENCIL_DEPTHS(X) X(1) X(2) X(4) X(6) X(8) X(12) X(16) X(32)
+#define GOLHIP_X(K)                                                                           \
+    hipError_t launch_stencil_k##K(int variant, const uint32_t *in, uint32_t *out,            \
+                                   const StencilParams &p, unsigned long long *slots,        \
+                                   hipStream_t s);                                           \
+    const void *stencil_fn_k##K(int variant);
+GOLHIP_STENCIL_DEPTHS(GOLHIP_X)
+#undef GOLHIP_X
+
+// Tuning knob (GOLHIP_LDS_PAD = bytes of unused dynamic LDS per block): caps the resident blocks
+// per CU, to measure the stencil's sensitivity to occupancy.  0 in production.
+inline size_t lds_pad_bytes() {
+    const char *e = std::getenv("GOLHIP_LDS_PAD");
+    return e ? (size_t)std::atol(e) : (size_t)0;
 }
 
 // Launch the K-generation stencil (K in {1,2,4,6,8,12,16,32}). count_slots (nullable) receives

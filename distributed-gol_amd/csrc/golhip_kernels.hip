@@ -1,778 +1,18 @@
-// golhip_kernels.hip -- hand-written gfx950 (CDNA4, wave64) kernels of libgolhip.
-//
-// Hot path: gol_stencil<K>, a temporally blocked, bit-sliced B3/S23 stencil on a 1-bit-per-cell
-// torus.  It replaces the reference's per-cell worker loop
-//   calculateNextState / updateCell / countAliveCellsAdjacent   server/server.go:21-75
-// and the per-turn alive scan calculateAliveCells (gol/distributor.go:153-166,186) is fused into
-// it as a per-generation popcount.
-//
-// Mapping (see DESIGN.md for the roofline):
-//   * one lane = one 32-bit word (32 cells) of a row; a wave = 64 consecutive words of a row.
-//     The outer bits of lanes 0 and 63 go stale one bit per generation (their outer neighbour
-//     is outside the wave): for K <= 16 lane 0 still owns its upper and lane 63 its lower half
-//     word (63 words per wave), for K <= 32 lanes 0 and 63 are pure halo (62 words per wave);
-//   * horizontal neighbours cross lanes with DPP and are merged with v_alignbit; the production
-//     variant (DR) uses drifting row sums, which need only the west neighbour: one DPP + 2
-//     v_alignbit per row, the sums and the rule are v_bitop3 (gfx950): 12 VALU per word per
-//     generation (13 with the two-sided sums);
-//   * each wave streams down a band of rows keeping, per generation level, the last two rows'
-//     (sum, carry, cell) in registers: one input row in -> one row out per level per step, so a
-//     launch advances K generations while reading the board once and writing it once.
+// golhip_kernels.hip -- the supporting gfx950 kernels of libgolhip (counts finalize, PGM pack /
+// unpack, random init, popcount, alive-cell / flip extraction, word I/O) and the dispatchers of
+// the hot-path stencil, whose kernels live in golhip_stencil.hpp (one TU per launch depth:
+// stencil_k*.hip, stencil_split.hip).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <algorithm>
 #include <cstdlib>
-#include <type_traits>
-#include <utility>
 
 #include "golhip_internal.hpp"
 
 namespace golhip {
 namespace {
 
-__device__ __forceinline__ uint32_t lane_from_west(uint32_t v) {  // lane i <- lane i-1
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138 /* wave_shr:1 */, 0xf, 0xf, false);
-}
-__device__ __forceinline__ uint32_t lane_from_east(uint32_t v) {  // lane i <- lane i+1
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130 /* wave_shl:1 */, 0xf, 0xf, false);
-}
-
-// v_bitop3_b32 (gfx950): any 3-input boolean function in one VALU op.  The immediate is the
-// truth table indexed by (s0 << 2) | (s1 << 1) | s2, i.e. f(0xF0, 0xCC, 0xAA).
-#define GOL_TT(EXPR) ((uint8_t)([](uint32_t a, uint32_t b, uint32_t c) { return (EXPR); }(0xF0u, 0xCCu, 0xAAu)))
-#define GOL_BOP3(A, B, C, TT) __builtin_amdgcn_bitop3_b32((A), (B), (C), (TT))
-constexpr uint8_t kXor3 = GOL_TT(a ^ b ^ c);                          // 0x96
-constexpr uint8_t kMaj = GOL_TT((a & b) | (c & (a | b)));             // 0xE8
-constexpr uint8_t kTwosEven = GOL_TT(~(a | b | c) | (~a & ~b & c) | (a & b & ~c));  // k,p,q
-constexpr uint8_t kOddSelect = GOL_TT((a & ~b) | (~a & c));                    // o ? !q : mc
-static_assert(kTwosEven == 0x43 && kOddSelect == 0x3a, "bitop3 truth tables");
-
-// D consecutive 32-bit words of one row held by one lane (D = 1 or 2).
-template <int D>
-struct Words {
-    uint32_t w[D];
-};
-
-// Neighbour words of a lane's row: by DPP from lanes -1 / +1 (NoNb), or given (Nb: level 0 reads
-// them next to its own word from the LDS-DMA ring, saving the two cross-lane moves).
-struct NoNb {};
-struct Nb {
-    uint32_t wl, el;  // the word west of the lane's first word, east of its last word
-};
-
-// Horizontal 3-cell sums (west + self + east) of a lane's D words as sum bits s and carries cy.
-// The lane's outer neighbour words come from lanes -1 / +1 (one per side per row, so D = 2
-// halves the cross-lane ops per word); the 1-bit shifts are v_alignbit funnel shifts.
-template <int D, class N = NoNb>
-__device__ __forceinline__ void row_sum3(const Words<D> &c, Words<D> &s, Words<D> &cy,
-                                         const N &nb = N{}) {
-    uint32_t wl, el;
-    if constexpr (std::is_same_v<N, Nb>) {
-        wl = nb.wl;
-        el = nb.el;
-    } else {
-        wl = lane_from_west(c.w[D - 1]);
-        el = lane_from_east(c.w[0]);
-    }
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-        const uint32_t left = d == 0 ? wl : c.w[d - 1];
-        const uint32_t right = d == D - 1 ? el : c.w[d + 1];
-        const uint32_t w = __builtin_amdgcn_alignbit(c.w[d], left, 31);  // cell x-1 onto x
-        const uint32_t e = __builtin_amdgcn_alignbit(right, c.w[d], 1);  // cell x+1 onto x
-        s.w[d] = GOL_BOP3(w, c.w[d], e, kXor3);
-        cy.w[d] = GOL_BOP3(w, c.w[d], e, kMaj);
-    }
-}
-
-// Drifting 3-cell sums (DR variants, D = 1): only the WEST neighbour word is needed.  Position P
-// of the result holds the sum of cells P-2, P-1, P of the input, i.e. the sum centred on cell
-// P-1, and the centre cell P-1 itself (ctr): each generation moves the row one bit east in the
-// lane's frame, so a level costs one cross-lane move instead of two.  Nothing is lost at the east
-// edge (position 63*32+31 needs nothing beyond its own lane); the west edge goes stale two bits
-// per generation instead of one bit at each edge, the same cells in total.
-template <class N = NoNb>
-__device__ __forceinline__ void row_sum3_drift(uint32_t c, uint32_t &s, uint32_t &cy,
-                                               uint32_t &ctr, const N &nb = N{}) {
-    uint32_t wl;
-    if constexpr (std::is_same_v<N, Nb>)
-        wl = nb.wl;
-    else
-        wl = lane_from_west(c);
-    const uint32_t w1 = __builtin_amdgcn_alignbit(c, wl, 31);  // cell x-1 onto x
-    const uint32_t w2 = __builtin_amdgcn_alignbit(c, wl, 30);  // cell x-2 onto x
-    s = GOL_BOP3(w2, w1, c, kXor3);
-    cy = GOL_BOP3(w2, w1, c, kMaj);
-    ctr = w1;
-}
-
-// B3/S23 from three rows' 3-cell sums: S9 = 9-cell sum including the centre cell mc;
-// alive next iff S9 == 3, or S9 == 4 and the cell is alive (server/server.go:35-52).
-// S9 = o + 2T with T = k + p + 2q (o,k: full adder of the sum bits, p,q: of the carries).
-//   o = 1: next iff T == 1, i.e. q = 0 and T != 0, 2;     o = 0: next iff mc and T in {0, 2}
-//   (T == 0 with mc alive cannot happen: mc is part of S9).
-// With u = [T in {0,2}] and v = o ? !q : mc this is next = v & (o ^ u): 7 v_bitop3 per word,
-// u and v independent (found by exhaustive search over 3-gate circuits on o,k,p,q,mc).
-__device__ __forceinline__ uint32_t life_next(uint32_t as, uint32_t acy, uint32_t ms,
-                                              uint32_t mcy, uint32_t mc, uint32_t bs,
-                                              uint32_t bcy) {
-    const uint32_t o = GOL_BOP3(as, ms, bs, kXor3);    // S9 bit 0
-    const uint32_t k = GOL_BOP3(as, ms, bs, kMaj);     // carry into the twos
-    const uint32_t p = GOL_BOP3(acy, mcy, bcy, kXor3);
-    const uint32_t q = GOL_BOP3(acy, mcy, bcy, kMaj);
-    const uint32_t u = GOL_BOP3(k, p, q, kTwosEven);
-    const uint32_t v = GOL_BOP3(o, q, mc, kOddSelect);
-    return GOL_BOP3(v, o, u, GOL_TT(a & (b ^ c)));
-}
-
-// A row's per-level state: 3-cell sum, carry and the cells themselves.
-template <int D>
-struct RowState {
-    Words<D> s, cy, c;
-};
-
-// One level update: `in` is the new row (below), `above`/`mid` the two previous rows of the level.
-// Writes the next generation of `mid` to nx and stores `in`'s state into `above` (now free).
-// DR: drifting sums (row_sum3_drift); the state keeps the drifted centre cells.
-template <int D, bool DR = false, class N = NoNb>
-__device__ __forceinline__ void level_update(RowState<D> &above, const RowState<D> &mid,
-                                             const Words<D> &in, Words<D> &nx, const N &nb = N{}) {
-    Words<D> ns, ncy, nc = in;
-    if constexpr (DR) {
-        static_assert(D == 1, "drift needs one word per lane");
-        row_sum3_drift<N>(in.w[0], ns.w[0], ncy.w[0], nc.w[0], nb);
-    } else {
-        row_sum3<D>(in, ns, ncy, nb);
-    }
-#pragma unroll
-    for (int d = 0; d < D; ++d)
-        nx.w[d] = life_next(above.s.w[d], above.cy.w[d], mid.s.w[d], mid.cy.w[d], mid.c.w[d],
-                            ns.w[d], ncy.w[d]);
-    above.s = ns;
-    above.cy = ncy;
-    above.c = nc;
-}
-
-template <int D>
-__device__ __forceinline__ Words<D> load_words(const uint32_t *p) {
-    Words<D> v;
-    if constexpr (D == 2) {
-        const uint2 t = *reinterpret_cast<const uint2 *>(p);
-        v.w[0] = t.x;
-        v.w[1] = t.y;
-    } else {
-        v.w[0] = *p;
-    }
-    return v;
-}
-
-// Raw buffer store of a lane's D words: an offset past the descriptor's range is dropped by the
-// hardware, which is how halo lanes and pipeline-fill steps skip their store WITHOUT a branch
-// (a branch around the store would make the waitcnt pass count conservatively and shorten the
-// load prefetch distance).
-constexpr uint32_t kBufferRsrcWord3 = 0x00020000;  // gfx9-family raw buffer, 32-bit dwords
-constexpr int kOutOfRange = 0x40000000;
-template <int D>
-__device__ __forceinline__ void buffer_store_words(__amdgpu_buffer_rsrc_t r, int off,
-                                                   const Words<D> &v) {
-    if constexpr (D == 2) {
-        typedef int v2i __attribute__((ext_vector_type(2)));
-        v2i x = {(int)v.w[0], (int)v.w[1]};
-        __builtin_amdgcn_raw_buffer_store_b64(x, r, off, 0, 0);
-    } else {
-        __builtin_amdgcn_raw_buffer_store_b32((int)v.w[0], r, off, 0, 0);
-    }
-}
-
-template <int... I, class F>
-__device__ __forceinline__ void static_for(std::integer_sequence<int, I...>, F &&f) {
-    (f(std::integral_constant<int, I>{}), ...);
-}
-
-// Level update without the rule: only ingests the new row's 3-cell sums into the ring (pipeline
-// fill: the level's output would be garbage, but the rows it holds are needed two steps later).
-template <int D, bool DR = false, class N = NoNb>
-__device__ __forceinline__ void level_ingest(RowState<D> &above, const Words<D> &in,
-                                             const N &nb = N{}) {
-    if constexpr (DR) {
-        row_sum3_drift<N>(in.w[0], above.s.w[0], above.cy.w[0], above.c.w[0], nb);
-    } else {
-        row_sum3<D>(in, above.s, above.cy, nb);
-        above.c = in;
-    }
-}
-
-// Output rows [ya, yb) of band `bandi` of a launch (range 0 bands first, then range 1).
-// Row indices fit in 32 bits; keeping every loop-carried counter 32-bit keeps the compares on the
-// SALU (gfx9 has no 64-bit signed s_cmp, a 64-bit compare would drag them into VGPRs).
-__device__ __forceinline__ void band_rows(const StencilParams &p, int64_t bandi, int &ya, int &yb) {
-    if (bandi < p.nbands0) {
-        ya = (int)(p.r0b + bandi * p.band);
-        yb = (int)min((int64_t)ya + p.band, p.r0e);
-    } else {
-        ya = (int)(p.r1b + (bandi - p.nbands0) * p.band);
-        yb = (int)min((int64_t)ya + p.band, p.r1e);
-    }
-}
-
-// Input row stream of a band: rows ya-K, ya-K+1, ... wrapped mod H (single strip holding the
-// torus) or clamped to the halo'd strip [lo, hi).  Branch-free (scalar selects), so the waitcnt
-// pass sees one straight line of loads and stores and keeps the full prefetch distance.
-struct RowStream {
-    int ly, wrap, hi;
-    __device__ __forceinline__ RowStream(const StencilParams &p, int first) {
-        wrap = (int)p.wrap_rows;
-        hi = (int)p.hi;
-        const int lo = (int)p.lo;
-        ly = first;
-        if (wrap > 0) {
-            ly %= wrap;
-            if (ly < 0) ly += wrap;
-        } else {
-            ly = ly < lo ? lo : (ly >= hi ? hi - 1 : ly);
-        }
-    }
-    __device__ __forceinline__ void advance() {
-        const int nx = ly + 1;
-        ly = wrap > 0 ? (nx == wrap ? 0 : nx) : (nx < hi ? nx : hi - 1);
-    }
-};
-
-// Where a lane stores its (first) word: through at most one of a full store (off_full), the low
-// half (off_lo) or the high half (off_hi, HH only); the others point past the buffer descriptor
-// and are dropped.  own_mask: the owned cells of the word, for the counts.
-struct LaneStore {
-    int off_full = kOutOfRange, off_lo = kOutOfRange, off_hi = kOutOfRange;
-    uint32_t own_mask = 0;
-};
-template <bool HH>
-__device__ __forceinline__ LaneStore lane_store(int lane, int colraw, int col, int wd) {
-    LaneStore o;
-    if (HH) {
-        // owned unwrapped cells: [-16, 32wd - 16); lane 0 -> upper half, lane 63 -> lower half
-        const int last = wd - 1;
-        if (lane == 0) {
-            if (colraw <= last - 1) { o.off_hi = col * 4 + 2; o.own_mask = 0xffff0000u; }
-        } else if (lane == 63) {
-            if (colraw <= last) { o.off_lo = col * 4; o.own_mask = 0x0000ffffu; }
-        } else if (colraw < last) {
-            o.off_full = col * 4; o.own_mask = ~0u;
-        } else if (colraw == last) {
-            o.off_lo = col * 4; o.own_mask = 0x0000ffffu;
-        }
-    } else if (lane >= 1 && lane <= 62 && colraw < wd) {
-        o.off_full = col * 4;
-        o.own_mask = ~0u;
-    }
-    return o;
-}
-
-template <int D, bool HH>
-__device__ __forceinline__ void store_row(__amdgpu_buffer_rsrc_t r, const LaneStore &ls,
-                                          const Words<D> &v, int rowoff) {
-    buffer_store_words<D>(r, ls.off_full + rowoff, v);
-    if (HH) {
-        __builtin_amdgcn_raw_buffer_store_b16((short)v.w[0], r, ls.off_lo + rowoff, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b16((short)(v.w[0] >> 16), r, ls.off_hi + rowoff, 0, 0);
-    }
-}
-
-// Per-level alive counts of a wave -> its spread slot of each generation (agent-scope atomics).
-template <int NL>
-__device__ __forceinline__ void flush_counts(const uint32_t (&acc)[NL], int j0, int lane,
-                                             int64_t wave, unsigned long long *slots) {
-#pragma unroll
-    for (int j = 0; j < NL; ++j) {
-        uint32_t v = acc[j];
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-        if (lane == 0 && v)
-            __hip_atomic_fetch_add(&slots[(j0 + j) * kCountSlots + (int)(wave & (kCountSlots - 1))],
-                                   (unsigned long long)v, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-// Column geometry of a wave's 64 lanes (shared with the host via chunk_words()):
-//   default : lanes 1..62 own D words each, lanes 0 and 63 are the horizontal halo (K <= 32);
-//   HH      : (D = 1, K <= 16) a halo needs only K <= 16 bits, so lane 0 owns the upper and lane 63
-//             the lower half of its word: 63 words per wave, chunk c owns cells
-//             [2016c - 16, 2016(c+1) - 16) (unwrapped), stored as full words plus two halves.
-// The hot kernel.  K = generations per launch, D = words per lane.
-// SKEW = false: the K levels of one step form one dependent chain (level j+1 consumes the row
-//               level j produced in the same step).
-// SKEW = true : level j consumes the row level j-1 produced in the PREVIOUS step, so the K level
-//               updates of a step are independent (K-way ILP); the pipeline is K-1 steps deeper.
-// DR = true: drifting row sums (row_sum3_drift, one cross-lane move per level update instead of
-//             two); level j's rows sit j+1 bits east in the lane frame, the stored level-K row is
-//             shifted back by one DPP + v_alignbit per stored word, and the per-level count masks
-//             follow the drift.  Needs the half-word halo geometry (D = 1, K <= 16, chained).
-template <int K, bool COUNT, bool SKEW, int D, int PF, bool HH, bool DR = false>
-__global__ __launch_bounds__(256) void gol_stencil(const uint32_t *__restrict__ in,
-                                                   uint32_t *__restrict__ out, StencilParams p,
-                                                   unsigned long long *__restrict__ slots) {
-    static_assert(!HH || (D == 1 && K <= 16), "half-word halo needs D = 1, K <= 16");
-    static_assert(!DR || (HH && !SKEW), "drift needs the half-word halo, chained levels");
-    const int lane = threadIdx.x & 63;
-    // wave index made provably uniform so every band/row quantity lives in SGPRs
-    const int64_t wave =
-        (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int64_t chunk = wave % p.nchunks;
-    const int64_t bandi = wave / p.nchunks;
-    if (bandi >= p.nbands) return;  // wave-uniform
-    int ya, yb;
-    band_rows(p, bandi, ya, yb);
-    // First word (unwrapped) of this lane and its wrapped column.
-    const int stride = HH ? 63 : 62 * D;
-    const int colraw = (int)chunk * stride + (lane - 1) * D;
-    const int col = (colraw + p.wd) % p.wd;
-    RowStream rows(p, ya - K);
-    auto load_next = [&]() -> Words<D> {
-        const Words<D> v = load_words<D>(in + (int64_t)rows.ly * p.pitch + col);
-        rows.advance();
-        return v;
-    };
-    // Output: one raw-buffer descriptor over the band's rows (offsets stay 32-bit for any board).
-    const int rowbytes = (int)(p.pitch * 4);
-    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
-        out + (int64_t)ya * p.pitch, 0, (yb - ya) * rowbytes, kBufferRsrcWord3);
-    const LaneStore ls = lane_store<HH>(lane, colraw, col, p.wd);
-    const uint32_t own_mask = ls.own_mask;
-    // DR counts need no per-level mask: level j's row sits d = j+1 bits east, so positions
-    // [32, 2048) (lanes 1..63 in full) hold cells [2016c - d, 2016(c+1) - d) of chunk c -- windows
-    // that tile the row at every level (valid: the drift leaves [2d, 2048) valid, 2d <= 32) -- and
-    // the last chunk's window ends at the row end (colraw < wd) for every d.  So every lane counts
-    // its whole word and the lanes outside the window drop their sums once, at the flush.
-    const bool count_lane = lane >= 1 && colraw < p.wd;
-    constexpr int NSTORE = HH ? 3 : 1;  // vector-memory stores per step
-    auto store_row = [&](const Words<D> &v, int rowoff) { golhip::store_row<D, HH>(orsrc, ls, v, rowoff); };
-
-    // Per level: a two-slot ring (X/Y swap roles every step) and, skewed, the pending input row.
-    RowState<D> X[K], Y[K];
-    Words<D> pend[K];
-    uint32_t acc[K];
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            X[j].s.w[d] = X[j].cy.w[d] = X[j].c.w[d] = 0;
-            Y[j].s.w[d] = Y[j].cy.w[d] = Y[j].c.w[d] = 0;
-            pend[j].w[d] = 0;
-        }
-        acc[j] = 0;
-    }
-    const int nrows = yb - ya;
-    const int lag = SKEW ? 3 * K - 1 : 2 * K;  // steps before the first stored row
-    const int nsteps = nrows + lag;
-
-    // One step: a new level-0 row enters, every level emits one row, the level-K row is stored.
-    // PAR 0: above = X, mid = Y, new -> X.  PAR 1: above = Y, mid = X, new -> Y.
-    // Chained: level j+1 takes level j's output of this step; level j's output row is
-    //   ya - K + st - (j+1), valid from step 2j+2 on (its above/mid rows arrive at steps 2j and
-    //   2j+1).  FILL = true (pipeline-fill steps only): level j is skipped before step 2j and only
-    //   ingests its input at steps 2j, 2j+1 -- the garbage rows of the fill are never computed.
-    // Skewed: levels in descending order, level j takes pend[j] (level j-1's output of the
-    //   previous step) and its output overwrites pend[j+1] after level j+1 has read it; level j's
-    //   output row is ya - K + st - 1 - 2j.
-    auto step = [&](auto par, auto fill, const Words<D> &vin, int st, const auto &nb0) {
-        constexpr int PAR = decltype(par)::value;
-        constexpr int FST = decltype(fill)::value;  // fill step index (compile time) or -1
-        constexpr bool FILL = FST >= 0 && !SKEW;
-        Words<D> nc = vin;
-#pragma unroll
-        for (int jj = 0; jj < K; ++jj) {
-            const int j = SKEW ? K - 1 - jj : jj;
-            const Words<D> lin = SKEW ? (j == 0 ? vin : pend[j]) : nc;
-            if (FILL && FST < 2 * j + 2) {  // folds away: FST and (unrolled) j are constants
-                if (FST >= 2 * j) {
-                    if (j == 0)
-                        level_ingest<D, DR>(PAR == 0 ? X[j] : Y[j], lin, nb0);
-                    else
-                        level_ingest<D, DR>(PAR == 0 ? X[j] : Y[j], lin);
-                }
-                if (j == K - 1) store_row(lin, kOutOfRange);  // keep the per-step store count
-                continue;
-            }
-            Words<D> nx;
-            if (j == 0)  // level 0 takes the new row with its given neighbours (if any)
-                level_update<D, DR>(PAR == 0 ? X[j] : Y[j], PAR == 0 ? Y[j] : X[j], lin, nx, nb0);
-            else
-                level_update<D, DR>(PAR == 0 ? X[j] : Y[j], PAR == 0 ? Y[j] : X[j], lin, nx);
-            if (COUNT) {
-                const int r = SKEW ? st - K - 1 - 2 * j : st - K - (j + 1);
-                const uint32_t m = DR ? ~0u : own_mask;  // DR: whole words, see count_lane
-                if (r >= 0 && r < nrows) acc[j] += __builtin_popcount(nx.w[0] & m) +
-                                                   (D == 2 ? __builtin_popcount(nx.w[D - 1] & own_mask) : 0);
-            }
-            if (j == K - 1) {
-                const int r = st - lag;  // stored row - ya
-                if constexpr (DR)  // back to the board frame: K bits west
-                    nx.w[0] = __builtin_amdgcn_alignbit(lane_from_east(nx.w[0]), nx.w[0], K);
-                store_row(nx, (r >= 0 && r < nrows) ? r * rowbytes : kOutOfRange);
-                if (PF) asm volatile("" ::: "memory");
-            } else if (SKEW) {
-                pend[j + 1] = nx;
-            } else {
-                nc = nx;
-            }
-        }
-    };
-    using Par0 = std::integral_constant<int, 0>;
-    using Par1 = std::integral_constant<int, 1>;
-    using Steady = std::integral_constant<int, -1>;
-
-    if constexpr (PF == 0) {
-        // Register prefetch ring: loads run P steps ahead of their use (deeper for small K,
-        // whose steps are short and would otherwise expose HBM latency).
-        constexpr int P = K >= 4 ? 4 : (K == 2 ? 8 : 16);
-        Words<D> buf[P];
-#pragma unroll
-        for (int u = 0; u < P; ++u) buf[u] = load_next();
-        for (int s = 0; s < nsteps; s += P) {
-#pragma unroll
-            for (int u = 0; u < P; ++u) {
-                const Words<D> vin = buf[u];
-                buf[u] = load_next();
-                if (u & 1)
-                    step(Par1{}, Steady{}, vin, s + u, NoNb{});
-                else
-                    step(Par0{}, Steady{}, vin, s + u, NoNb{});
-            }
-        }
-    } else {
-        // LDS ring filled by LDS-DMA (global_load_lds): no VGPR destination, so the prefetch
-        // distance costs no registers and no register moves.  A row chunk is D DMAs of 64
-        // consecutive words (lane L of DMA i fetches word base + 64i + L), read back as the
-        // lane's D consecutive words.  PL slots, PL-1 rows in flight: step st reads slot
-        // st % PL and refills the slot step st-1 read, AFTER an lgkmcnt(0) wait -- a DMA's LDS
-        // write is not ordered with this wave's earlier ds_reads, so a slot is only refilled once
-        // its reads have returned.  Each step waits (by hand: the compiler does not track LDS-DMA
-        // completion) until its row's DMAs have landed: a step issues D DMAs and NSTORE stores,
-        // so after the last DMA for step st-(PL-1) this wave issued NSTORE stores of that step and
-        // (D + NSTORE) ops for each of the PL-2 steps after it; the wait leaves a margin of 2.
-        // Deeper ring for K <= 2: steps are short, the launch is HBM-bound and needs more bytes
-        // in flight per CU.
-        constexpr int PL = K <= 2 ? 16 : 8;
-        constexpr int kWait = NSTORE + (D + NSTORE) * (PL - 2) - 2;
-        static_assert(kWait <= 63, "vmcnt field");
-        __shared__ __attribute__((aligned(16))) uint32_t ring[4][PL][64 * D];
-        const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-        const int nb_w = max(lane * D - 1, 0), nb_e = min(lane * D + D, 64 * D - 1);
-        int dcol[D];
-        {
-            const int base = (int)chunk * stride - D;
-#pragma unroll
-            for (int i = 0; i < D; ++i) dcol[i] = (base + 64 * i + lane + p.wd) % p.wd;
-        }
-        // Compiler-level fences (empty asm with a memory clobber) keep every DMA and store in
-        // program order, so the per-step vmcnt accounting holds whatever the scheduler does.
-        auto dma_next = [&](int slot) {
-            const uint32_t *row = in + (int64_t)rows.ly * p.pitch;
-#pragma unroll
-            for (int i = 0; i < D; ++i) {
-                __builtin_amdgcn_global_load_lds(row + dcol[i], &ring[w][slot][64 * i], 4, 0, 0);
-                asm volatile("" ::: "memory");
-            }
-            rows.advance();
-        };
-        Words<D> zero;
-#pragma unroll
-        for (int d = 0; d < D; ++d) zero.w[d] = 0;
-#pragma unroll
-        for (int u = 0; u < PL - 1; ++u) {
-            dma_next(u);
-            // dummy (dropped) stores keep the (DMA, stores) cadence; distinct offsets so no
-            // dead-store elimination merges them
-            store_row(zero, kOutOfRange + 8 * u);
-            asm volatile("" ::: "memory");
-        }
-        auto one_step = [&](int u, auto fill, int st) {
-            asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"(kWait) : "memory");
-            dma_next((u + PL - 1) % PL);
-            Words<D> vin;
-#pragma unroll
-            for (int d = 0; d < D; ++d) vin.w[d] = ring[w][u][lane * D + d];
-            // level 0's neighbour words straight from the ring (the row's lanes -1 / +1; the
-            // edge lanes read a clamped, garbage word: they are halo, as with DPP)
-            const Nb nb0{ring[w][u][nb_w], ring[w][u][nb_e]};
-            if (st & 1)
-                step(Par1{}, fill, vin, st, nb0);
-            else
-                step(Par0{}, fill, vin, st, nb0);
-        };
-        int s = 0;
-        // Pipeline fill of the chained levels (2K steps, fully unrolled so every level's
-        // skip / ingest-only / full decision is a compile-time constant: no branches, no extra
-        // registers).  Needs 2K to be a multiple of the ring depth so the main loop stays aligned.
-        if constexpr (!SKEW && (2 * K) % PL == 0) {
-            static_for(std::make_integer_sequence<int, 2 * K>{}, [&](auto stc) {
-                constexpr int ST = decltype(stc)::value;
-                one_step(ST % PL, stc, ST);
-            });
-            s = 2 * K;
-        }
-        for (; s < nsteps; s += PL) {
-#pragma unroll
-            for (int u = 0; u < PL; ++u) one_step(u, Steady{}, s + u);
-        }
-        // Drain the ring's in-flight DMAs before the wave can retire: a DMA landing after the
-        // workgroup released its LDS would write into the next workgroup's ring.
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-
-    if (COUNT) {
-        if (DR && !count_lane) {
-#pragma unroll
-            for (int j = 0; j < K; ++j) acc[j] = 0;
-        }
-        flush_counts<K>(acc, 0, lane, wave, slots);
-    }
-}
-
-// ---------------------------------------------------------------- one generation (K = 1)
-// K = 1 is HBM-bound (0.25 B per cell update against ~13 VALU per 32 cells), so it gets its own
-// memory-shaped kernel: a lane holds 4 consecutive words (one 16-byte load / store per row, 1 KiB
-// per wave instruction), a wave covers 256 words with NO halo lanes (one generation needs only
-// the single bit beyond each edge: lanes 0 and 63 load the word outside the wave as a 4-byte side
-// load, which DPP with bound_ctrl off leaves in place at the wave edge), so 65536-wide rows tile
-// into exactly 8 waves.  Rows stream through a register ring P rows deep; the row sums of the
-// row above and of the middle row stay in registers.  Lanes past the torus width hold the
-// wrapped words (the torus continuation), so partial last chunks need no special case; they
-// just do not store.
-// P = rows in flight per wave; NT bit 0 / bit 1 = non-temporal loads / stores (streamed once).
-template <bool COUNT, int P = 8, int NT = 0>
-__global__ __launch_bounds__(256) void gol_step1(const uint32_t *__restrict__ in,
-                                                 uint32_t *__restrict__ out, StencilParams p,
-                                                 unsigned long long *__restrict__ slots) {
-    const int lane = threadIdx.x & 63;
-    const int64_t wave =
-        (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int64_t chunk = wave % p.nchunks, bandi = wave / p.nchunks;
-    if (bandi >= p.nbands) return;
-    int ya, yb;
-    band_rows(p, bandi, ya, yb);
-    const int base = (int)chunk * 256;
-    const int colraw = base + lane * 4;  // unwrapped index of the lane's first word
-    const int col = colraw % p.wd;       // wd % 4 == 0: the 4 words never straddle the wrap
-    // side word: west of the wave (lane 0), east of it (lane 63); other lanes reload their own
-    // first word (same cache line, no extra traffic) so the load needs no branch
-    const int xcol = lane == 0 ? (base - 1 + p.wd) % p.wd : lane == 63 ? (base + 256) % p.wd : col;
-    const int nrows = yb - ya, nsteps = nrows + 2;
-    const int rowbytes = (int)(p.pitch * 4);
-    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
-        out + (int64_t)ya * p.pitch, 0, (yb - ya) * rowbytes, kBufferRsrcWord3);
-    const bool owned = colraw < p.wd;
-    const int off = owned ? col * 4 : kOutOfRange;
-
-    RowStream rows(p, ya - 1);
-    uint4 buf[P];
-    uint32_t xbuf[P];
-    auto load_next = [&](int u) {
-        const uint32_t *r = in + (int64_t)rows.ly * p.pitch;
-        if constexpr (NT & 1) {
-            typedef unsigned v4u __attribute__((ext_vector_type(4)));
-            const v4u t = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(r + col));
-            buf[u] = make_uint4(t.x, t.y, t.z, t.w);
-            xbuf[u] = __builtin_nontemporal_load(r + xcol);
-        } else {
-            buf[u] = *reinterpret_cast<const uint4 *>(r + col);
-            xbuf[u] = r[xcol];
-        }
-        rows.advance();
-    };
-#pragma unroll
-    for (int u = 0; u < P; ++u) load_next(u);
-
-    Words<4> as, acy, ms, mcy, mc;  // row sums of the row above and of the middle row + its cells
-#pragma unroll
-    for (int d = 0; d < 4; ++d) as.w[d] = acy.w[d] = ms.w[d] = mcy.w[d] = mc.w[d] = 0;
-    uint32_t acc = 0;
-    for (int s = 0; s < nsteps; s += P) {
-#pragma unroll
-        for (int u = 0; u < P; ++u) {
-            const int st = s + u;
-            Words<4> c;
-            c.w[0] = buf[u].x;
-            c.w[1] = buf[u].y;
-            c.w[2] = buf[u].z;
-            c.w[3] = buf[u].w;
-            const uint32_t x = xbuf[u];
-            load_next(u);
-            // neighbour words: lane L-1's last word / lane L+1's first word; at the wave edges the
-            // source lane does not exist and the side word x stays (bound_ctrl off keeps `old`)
-            const Nb nb{(uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)c.w[3], 0x138, 0xf, 0xf, false),
-                        (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)c.w[0], 0x130, 0xf, 0xf, false)};
-            Words<4> bs, bcy;
-            row_sum3<4>(c, bs, bcy, nb);
-            Words<4> nx;
-#pragma unroll
-            for (int d = 0; d < 4; ++d)
-                nx.w[d] = life_next(as.w[d], acy.w[d], ms.w[d], mcy.w[d], mc.w[d], bs.w[d], bcy.w[d]);
-            const int r = st - 2;  // the middle row, relative to ya
-            const bool live = r >= 0 && r < nrows;
-            typedef int v4i __attribute__((ext_vector_type(4)));
-            const v4i v = {(int)nx.w[0], (int)nx.w[1], (int)nx.w[2], (int)nx.w[3]};
-            __builtin_amdgcn_raw_buffer_store_b128(v, orsrc, off + (live ? r * rowbytes : kOutOfRange), 0,
-                                                   (NT & 2) ? 2 /* nt */ : 0);
-            if (COUNT && live && owned)
-                acc += __builtin_popcount(nx.w[0]) + __builtin_popcount(nx.w[1]) +
-                       __builtin_popcount(nx.w[2]) + __builtin_popcount(nx.w[3]);
-            as = ms;
-            acy = mcy;
-            ms = bs;
-            mcy = bcy;
-            mc = c;
-        }
-    }
-    if (COUNT) {
-        const uint32_t a[1] = {acc};
-        flush_counts<1>(a, 0, lane, wave, slots);
-    }
-}
-
-// ---------------------------------------------------------------- level-split stencil
-// Small boards are latency-bound: a round of minimal bands gives fewer waves than SIMDs, and a
-// lone wave's time is its dependent chain -- band*K level updates (+ the fill), K levels deep
-// per step.  gol_stencil_split spreads the K levels of one (band, chunk) over a workgroup of S
-// waves: wave R computes levels [R*K/S, (R+1)*K/S) and hands its last level's output row to wave
-// R+1 through LDS; the group steps in lockstep (one s_barrier per step), so every wave's chain is
-// K/S levels and the board runs S times as many waves, with no extra (halo) work.
-// Wave R's level j outputs row ya - K + st - (j+1) - R at step st (one step of delay per hand-off),
-// valid from step 2j + 2 + R; the final row (j = K-1, R = S-1) lags by 2K + S - 1 steps.
-template <int K, bool COUNT, int S, int R>
-__device__ __forceinline__ void split_role(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
-                                           const StencilParams &p,
-                                           unsigned long long *__restrict__ slots, int64_t group,
-                                           int lane, uint32_t (*xring)[2][64],
-                                           uint32_t (*ring)[64]) {
-    constexpr bool HH = K <= 16;
-    constexpr bool DR = HH;                 // drifting row sums (see gol_stencil)
-    constexpr int NL = K / S, J0 = R * NL;  // this wave's levels: [J0, J0 + NL)
-    constexpr int PL = 8;                   // LDS-DMA ring depth (wave 0)
-    constexpr int LAG = 2 * K + S - 1;
-    constexpr int FILL = (LAG + PL - 1) / PL * PL;  // unrolled fill steps (ring-aligned)
-    const int64_t chunk = group % p.nchunks, bandi = group / p.nchunks;
-    int ya, yb;
-    band_rows(p, bandi, ya, yb);
-    const int colraw = (int)chunk * (HH ? 63 : 62) + lane - 1;
-    const int col = (colraw + p.wd) % p.wd;
-    const int nrows = yb - ya, nsteps = nrows + LAG;
-    const int rowbytes = (int)(p.pitch * 4);
-    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
-        out + (int64_t)ya * p.pitch, 0, (yb - ya) * rowbytes, kBufferRsrcWord3);
-    const LaneStore ls = lane_store<HH>(lane, colraw, col, p.wd);
-    const bool count_lane = lane >= 1 && colraw < p.wd;  // DR count window (see gol_stencil)
-    RowStream rows(p, ya - K);
-
-    RowState<1> X[NL], Y[NL];
-    uint32_t acc[NL];
-#pragma unroll
-    for (int j = 0; j < NL; ++j) {
-        X[j].s.w[0] = X[j].cy.w[0] = X[j].c.w[0] = 0;
-        Y[j].s.w[0] = Y[j].cy.w[0] = Y[j].c.w[0] = 0;
-        acc[j] = 0;
-    }
-    auto dma_next = [&](int slot) {
-        __builtin_amdgcn_global_load_lds(in + (int64_t)rows.ly * p.pitch + col, &ring[slot][0], 4, 0, 0);
-        asm volatile("" ::: "memory");
-        rows.advance();
-    };
-    if (R == 0) {
-#pragma unroll
-        for (int u = 0; u < PL - 1; ++u) dma_next(u);
-    }
-    // One lockstep step: take the input row (DMA ring or the previous wave's hand-off), run this
-    // wave's levels (compile-time fill guards when FST >= 0), hand off or store, barrier.
-    auto step = [&](auto par, auto fill, int u, int st) {
-        constexpr int PAR = decltype(par)::value;
-        constexpr int FST = decltype(fill)::value;
-        Words<1> nc;
-        if (R == 0) {
-            // PL-1 rows in flight: this slot's DMA has PL-2 younger ones (margin of 2); refill
-            // the slot the previous step read (its read returned before that step's barrier)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PL - 2 - 2) : "memory");
-            dma_next((u + PL - 1) % PL);
-            nc.w[0] = ring[u][lane];
-        } else {
-            nc.w[0] = xring[R - 1][(st - 1) & 1][lane];
-        }
-#pragma unroll
-        for (int jl = 0; jl < NL; ++jl) {
-            const int j = J0 + jl;
-            if (FST >= 0 && FST < 2 * j + 2 + R) {  // folds away: FST and (unrolled) j constant
-                if (FST >= 2 * j + R) level_ingest<1, DR>(PAR == 0 ? X[jl] : Y[jl], nc);
-                nc.w[0] = 0;
-                continue;
-            }
-            Words<1> nx;
-            if (PAR == 0)
-                level_update<1, DR>(X[jl], Y[jl], nc, nx);
-            else
-                level_update<1, DR>(Y[jl], X[jl], nc, nx);
-            if (COUNT) {
-                const int rr = st - K - (j + 1) - R;
-                const uint32_t m = DR ? ~0u : ls.own_mask;
-                if (rr >= 0 && rr < nrows) acc[jl] += __builtin_popcount(nx.w[0] & m);
-            }
-            nc = nx;
-        }
-        if (R < S - 1) {
-            xring[R][st & 1][lane] = nc.w[0];
-        } else {
-            const int rr = st - LAG;
-            if constexpr (DR)  // back to the board frame: K bits west
-                nc.w[0] = __builtin_amdgcn_alignbit(lane_from_east(nc.w[0]), nc.w[0], K);
-            store_row<1, HH>(orsrc, ls, nc, (rr >= 0 && rr < nrows) ? rr * rowbytes : kOutOfRange);
-        }
-        // hand-off visible to the next wave, and this step's reads done before slots are reused
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    };
-    using Par0 = std::integral_constant<int, 0>;
-    using Par1 = std::integral_constant<int, 1>;
-    static_for(std::make_integer_sequence<int, FILL>{}, [&](auto stc) {
-        constexpr int ST = decltype(stc)::value;
-        if (ST & 1)
-            step(Par1{}, stc, ST % PL, ST);
-        else
-            step(Par0{}, stc, ST % PL, ST);
-    });
-    for (int s = FILL; s < nsteps; s += PL) {
-#pragma unroll
-        for (int u = 0; u < PL; ++u) {
-            if (u & 1)
-                step(Par1{}, std::integral_constant<int, -1>{}, u, s + u);
-            else
-                step(Par0{}, std::integral_constant<int, -1>{}, u, s + u);
-        }
-    }
-    if (R == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the ring
-    if (COUNT) {
-        if (DR && !count_lane) {
-#pragma unroll
-            for (int j = 0; j < NL; ++j) acc[j] = 0;
-        }
-        flush_counts<NL>(acc, J0, lane, group, slots);
-    }
-}
-
-template <int K, bool COUNT, int S>
-__global__ __launch_bounds__(64 * S) void gol_stencil_split(const uint32_t *__restrict__ in,
-                                                            uint32_t *__restrict__ out,
-                                                            StencilParams p,
-                                                            unsigned long long *__restrict__ slots) {
-    static_assert(S >= 2 && K % S == 0, "levels split evenly over S >= 2 waves");
-    __shared__ __attribute__((aligned(16))) uint32_t xring[S - 1][2][64];
-    __shared__ __attribute__((aligned(16))) uint32_t ring[8][64];
-    const int64_t group = blockIdx.x;
-    if (group / p.nchunks >= p.nbands) return;  // whole workgroup
-    const int lane = threadIdx.x & 63;
-    const int r = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    static_for(std::make_integer_sequence<int, S>{}, [&](auto rc) {
-        constexpr int RR = decltype(rc)::value;
-        if (r == RR) split_role<K, COUNT, S, RR>(in, out, p, slots, group, lane, xring, ring);
-    });
-}
 
 // Per-generation counts of a launch whose slots were not finalized in-kernel: block j sums
 // generation j's kCountSlots slots (one per lane) and re-zeroes them.
@@ -1018,7 +258,6 @@ __global__ void words_in(const uint64_t *__restrict__ words, int64_t rows, int64
         row0[y * pitch + col] = (col & 1) ? (uint32_t)(w >> 32) : (uint32_t)w;
     }
 }
-
 inline unsigned grid_for(int64_t n, int threads = 256, int64_t cap = 8192) {
     int64_t g = (n + threads - 1) / threads;
     if (g < 1) g = 1;
@@ -1026,168 +265,20 @@ inline unsigned grid_for(int64_t n, int threads = 256, int64_t cap = 8192) {
     return (unsigned)g;
 }
 
-// Tuning knob (GOLHIP_LDS_PAD = bytes of unused dynamic LDS per block): caps the resident blocks
-// per CU, to measure the stencil's sensitivity to occupancy.  0 in production.
-inline size_t lds_pad_bytes() {
-    static const size_t pad = [] {
-        const char *e = std::getenv("GOLHIP_LDS_PAD");
-        return e ? (size_t)std::atol(e) : (size_t)0;
-    }();
-    return pad;
-}
-
-template <int K, int D>
-constexpr bool kHalfHalo = D == 1 && K <= 16;  // keep in sync with chunk_words()
-
-// Tuning knob GOLHIP_STEP1 = P*10 + NT selects gol_step1's prefetch depth and cache policy
-// (read once; unset = the production configuration).
-inline int step1_config() {
-    static const int cfg = [] {
-        const char *e = std::getenv("GOLHIP_STEP1");
-        return e ? std::atoi(e) : 42;
-    }();
-    return cfg;
-}
-template <int P, int NT>
-hipError_t launch_step1_cfg(const uint32_t *in, uint32_t *out, const StencilParams &p,
-                            unsigned long long *slots, hipStream_t s) {
-    const unsigned blocks = (unsigned)((p.nbands * (int64_t)p.nchunks + 3) / 4);
-    if (blocks == 0) return hipSuccess;
-    if (slots)
-        hipLaunchKernelGGL((gol_step1<true, P, NT>), dim3(blocks), dim3(256), 0, s, in, out, p, slots);
-    else
-        hipLaunchKernelGGL((gol_step1<false, P, NT>), dim3(blocks), dim3(256), 0, s, in, out, p, slots);
-    return hipGetLastError();
-}
-#define GOLHIP_STEP1_CONFIGS(X) \
-    X(20, 2, 0) X(22, 2, 2) X(30, 3, 0) X(32, 3, 2) X(40, 4, 0) X(41, 4, 1) X(42, 4, 2) \
-    X(43, 4, 3) X(60, 6, 0) X(62, 6, 2) X(80, 8, 0) X(82, 8, 2)
-inline hipError_t launch_step1(const uint32_t *in, uint32_t *out, const StencilParams &p,
-                               unsigned long long *slots, hipStream_t s) {
-    switch (step1_config()) {
-#define GOLHIP_X(C, P, NT) \
-    case C: return launch_step1_cfg<P, NT>(in, out, p, slots, s);
-        GOLHIP_STEP1_CONFIGS(GOLHIP_X)
-#undef GOLHIP_X
-        default: return launch_step1_cfg<4, 2>(in, out, p, slots, s);
-    }
-}
-inline const void *step1_fn() {
-    switch (step1_config()) {
-#define GOLHIP_X(C, P, NT) \
-    case C: return (const void *)gol_step1<false, P, NT>;
-        GOLHIP_STEP1_CONFIGS(GOLHIP_X)
-#undef GOLHIP_X
-        default: return (const void *)gol_step1<false, 4, 2>;
-    }
-}
-
-template <int K, bool SKEW, int D, int PF = 0, bool DR = false>
-hipError_t launch_stencil_k(const uint32_t *in, uint32_t *out, const StencilParams &p,
-                            unsigned long long *slots, hipStream_t s) {
-    const int64_t waves = p.nbands * (int64_t)p.nchunks;
-    const unsigned blocks = (unsigned)((waves + 3) / 4);
-    if (blocks == 0) return hipSuccess;
-    if (slots)
-        hipLaunchKernelGGL((gol_stencil<K, true, SKEW, D, PF, kHalfHalo<K, D>, DR>), dim3(blocks), dim3(256),
-                           lds_pad_bytes(), s, in, out, p, slots);
-    else
-        hipLaunchKernelGGL((gol_stencil<K, false, SKEW, D, PF, kHalfHalo<K, D>, DR>), dim3(blocks), dim3(256),
-                           lds_pad_bytes(), s, in, out, p, slots);
-    return hipGetLastError();
-}
-
-template <int K>
-hipError_t launch_variant(int variant, const uint32_t *in, uint32_t *out, const StencilParams &p,
-                          unsigned long long *slots, hipStream_t s) {
-    switch (variant) {
-        case kVariantChain: return launch_stencil_k<K, false, 1>(in, out, p, slots, s);
-        case kVariantSkewD2: return launch_stencil_k<K, true, 2>(in, out, p, slots, s);
-        case kVariantChainD2: return launch_stencil_k<K, false, 2>(in, out, p, slots, s);
-        case kVariantSkewLdsPf: return launch_stencil_k<K, true, 1, 1>(in, out, p, slots, s);
-        case kVariantChainLdsPf:
-            if constexpr (K == 1) return launch_step1(in, out, p, slots, s);  // production K = 1
-            return launch_stencil_k<K, false, 1, 1>(in, out, p, slots, s);
-        case kVariantSkewLdsD2: return launch_stencil_k<K, true, 2, 1>(in, out, p, slots, s);
-        case kVariantChainLdsD2: return launch_stencil_k<K, false, 2, 1>(in, out, p, slots, s);
-        case kVariantDriftLds:
-            if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
-            else if constexpr (K > 16) return launch_stencil_k<K, false, 1, 1>(in, out, p, slots, s);
-            else return launch_stencil_k<K, false, 1, 1, true>(in, out, p, slots, s);
-        default: return launch_stencil_k<K, true, 1>(in, out, p, slots, s);
-    }
-}
-
-template <int K>
-const void *variant_fn(int variant) {
-    switch (variant) {
-        case kVariantChain: return (const void *)gol_stencil<K, false, false, 1, 0, kHalfHalo<K, 1>>;
-        case kVariantSkewD2: return (const void *)gol_stencil<K, false, true, 2, 0, kHalfHalo<K, 2>>;
-        case kVariantChainD2: return (const void *)gol_stencil<K, false, false, 2, 0, kHalfHalo<K, 2>>;
-        case kVariantSkewLdsPf: return (const void *)gol_stencil<K, false, true, 1, 1, kHalfHalo<K, 1>>;
-        case kVariantChainLdsPf:
-            if constexpr (K == 1) return step1_fn();
-            return (const void *)gol_stencil<K, false, false, 1, 1, kHalfHalo<K, 1>>;
-        case kVariantSkewLdsD2: return (const void *)gol_stencil<K, false, true, 2, 1, kHalfHalo<K, 2>>;
-        case kVariantChainLdsD2: return (const void *)gol_stencil<K, false, false, 2, 1, kHalfHalo<K, 2>>;
-        case kVariantDriftLds:
-            if constexpr (K == 1) return step1_fn();
-            else return (const void *)gol_stencil<K, false, false, 1, 1, kHalfHalo<K, 1>, (K <= 16)>;
-        default: return (const void *)gol_stencil<K, false, true, 1, 0, kHalfHalo<K, 1>>;
-    }
-}
-
-template <int K, int S>
-hipError_t launch_split_ks(const uint32_t *in, uint32_t *out, const StencilParams &p,
-                           unsigned long long *slots, hipStream_t s) {
-    const unsigned blocks = (unsigned)(p.nbands * (int64_t)p.nchunks);
-    if (blocks == 0) return hipSuccess;
-    if (slots)
-        hipLaunchKernelGGL((gol_stencil_split<K, true, S>), dim3(blocks), dim3(64 * S), 0, s, in,
-                           out, p, slots);
-    else
-        hipLaunchKernelGGL((gol_stencil_split<K, false, S>), dim3(blocks), dim3(64 * S), 0, s, in,
-                           out, p, slots);
-    return hipGetLastError();
-}
-
 }  // namespace
-
-bool stencil_split_supported(int K, int S) {
-    if (S == 2) return K == 4 || K == 6 || K == 8 || K == 12 || K == 16 || K == 32;
-    if (S == 4) return K == 4 || K == 8 || K == 12 || K == 16 || K == 32;
-    if (S == 8) return K == 8 || K == 16 || K == 32;
-    return false;
-}
-
-hipError_t launch_stencil_split(int K, int S, const uint32_t *in_row0, uint32_t *out_row0,
-                                const StencilParams &p, unsigned long long *slots, hipStream_t s) {
-#define GOL_SPLIT_CASE(KK, SS) \
-    if (K == KK && S == SS) return launch_split_ks<KK, SS>(in_row0, out_row0, p, slots, s);
-    GOL_SPLIT_CASE(4, 2) GOL_SPLIT_CASE(6, 2) GOL_SPLIT_CASE(8, 2) GOL_SPLIT_CASE(12, 2)
-    GOL_SPLIT_CASE(16, 2) GOL_SPLIT_CASE(32, 2)
-    GOL_SPLIT_CASE(4, 4) GOL_SPLIT_CASE(8, 4) GOL_SPLIT_CASE(12, 4) GOL_SPLIT_CASE(16, 4)
-    GOL_SPLIT_CASE(32, 4)
-    GOL_SPLIT_CASE(8, 8) GOL_SPLIT_CASE(16, 8) GOL_SPLIT_CASE(32, 8)
-#undef GOL_SPLIT_CASE
-    return hipErrorInvalidValue;
-}
 
 bool stencil_k_supported(int K) {
     return K == 1 || K == 2 || K == 4 || K == 6 || K == 8 || K == 12 || K == 16 || K == 32;
 }
 
+// The per-depth stencil launchers live in stencil_k<K>.hip (one TU per depth).
 hipError_t launch_stencil(int K, int variant, const uint32_t *in_row0, uint32_t *out_row0,
                           const StencilParams &p, unsigned long long *slots, hipStream_t s) {
     switch (K) {
-        case 1: return launch_variant<1>(variant, in_row0, out_row0, p, slots, s);
-        case 2: return launch_variant<2>(variant, in_row0, out_row0, p, slots, s);
-        case 4: return launch_variant<4>(variant, in_row0, out_row0, p, slots, s);
-        case 6: return launch_variant<6>(variant, in_row0, out_row0, p, slots, s);
-        case 12: return launch_variant<12>(variant, in_row0, out_row0, p, slots, s);
-        case 8: return launch_variant<8>(variant, in_row0, out_row0, p, slots, s);
-        case 16: return launch_variant<16>(variant, in_row0, out_row0, p, slots, s);
-        case 32: return launch_variant<32>(variant, in_row0, out_row0, p, slots, s);
+#define GOLHIP_X(KK) \
+    case KK: return launch_stencil_k##KK(variant, in_row0, out_row0, p, slots, s);
+        GOLHIP_STENCIL_DEPTHS(GOLHIP_X)
+#undef GOLHIP_X
         default: return hipErrorInvalidValue;
     }
 }
@@ -1195,14 +286,10 @@ hipError_t launch_stencil(int K, int variant, const uint32_t *in_row0, uint32_t 
 int stencil_waves_per_cu(int K, int variant) {
     const void *fn = nullptr;
     switch (K) {
-        case 1: fn = variant_fn<1>(variant); break;
-        case 2: fn = variant_fn<2>(variant); break;
-        case 4: fn = variant_fn<4>(variant); break;
-        case 6: fn = variant_fn<6>(variant); break;
-        case 12: fn = variant_fn<12>(variant); break;
-        case 8: fn = variant_fn<8>(variant); break;
-        case 16: fn = variant_fn<16>(variant); break;
-        case 32: fn = variant_fn<32>(variant); break;
+#define GOLHIP_X(KK) \
+    case KK: fn = stencil_fn_k##KK(variant); break;
+        GOLHIP_STENCIL_DEPTHS(GOLHIP_X)
+#undef GOLHIP_X
         default: return 4;
     }
     int blocks = 0;

@@ -1,0 +1,6 @@
+// stencil_k12.hip -- the 12-generation stencil launchers (every variant), one TU per launch depth.
+#include "golhip_stencil.hpp"
+
+namespace golhip {
+GOLHIP_DEFINE_STENCIL_K(12)
+}  // namespace golhip

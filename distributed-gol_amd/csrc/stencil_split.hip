@@ -1,0 +1,26 @@
+// stencil_split.hip -- the level-split stencil (small boards) launchers.
+#include "golhip_stencil.hpp"
+
+namespace golhip {
+
+bool stencil_split_supported(int K, int S) {
+    if (S == 2) return K == 4 || K == 6 || K == 8 || K == 12 || K == 16 || K == 32;
+    if (S == 4) return K == 4 || K == 8 || K == 12 || K == 16 || K == 32;
+    if (S == 8) return K == 8 || K == 16 || K == 32;
+    return false;
+}
+
+hipError_t launch_stencil_split(int K, int S, const uint32_t *in_row0, uint32_t *out_row0,
+                                const StencilParams &p, unsigned long long *slots, hipStream_t s) {
+#define GOL_SPLIT_CASE(KK, SS) \
+    if (K == KK && S == SS) return launch_split_ks<KK, SS>(in_row0, out_row0, p, slots, s);
+    GOL_SPLIT_CASE(4, 2) GOL_SPLIT_CASE(6, 2) GOL_SPLIT_CASE(8, 2) GOL_SPLIT_CASE(12, 2)
+    GOL_SPLIT_CASE(16, 2) GOL_SPLIT_CASE(32, 2)
+    GOL_SPLIT_CASE(4, 4) GOL_SPLIT_CASE(8, 4) GOL_SPLIT_CASE(12, 4) GOL_SPLIT_CASE(16, 4)
+    GOL_SPLIT_CASE(32, 4)
+    GOL_SPLIT_CASE(8, 8) GOL_SPLIT_CASE(16, 8) GOL_SPLIT_CASE(32, 8)
+#undef GOL_SPLIT_CASE
+    return hipErrorInvalidValue;
+}
+
+}  // namespace golhip

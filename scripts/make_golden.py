@@ -2,9 +2,10 @@
 """Generate the golden vectors of the synthetic configs with the (pinned) CPU oracle.
 
   cfg2: 5120x5120 random p=0.5 seed 2, per-turn alive counts for 10000 turns + final digest
-  cfg3: 65536x65536 random p=0.5 seed 3, per-turn counts for 1000 turns + digests at 8/1000
-  cfg5: 4096x4096 Gosper gun at (64,64) + R-pentomino at (2048,2048), counts for the first
-        100000 turns (SHA-256 of the uint32 array, every 1000th count listed)
+  cfg3: 65536x65536 random p=0.5 seed 3, per-turn counts for 1000 turns (CSV) + digests at 8/1000
+  cfg4: 262144x262144 random p=0.5 seed 4, per-turn counts for 176 turns (CSV) + digests at 16/176
+  cfg5: 4096x4096 Gosper gun at (64,64) + R-pentomino at (2048,2048), all 1e6 per-turn counts
+        (SHA-256 of the uint32 array; the array itself as a compressed delta npz) + digests
 Digests = SHA-256 of the packed little-endian uint64 rows (oracle.digest_words).
 Run from the repo root: python scripts/make_golden.py [cfg2|cfg3|cfg5 ...]
 """
@@ -35,6 +36,11 @@ def cfg2():
                      "oracle_seconds": round(time.time() - t, 1)}}
 
 
+def write_counts_csv(name, counts):
+    (OUT / name).write_text(
+        "completed_turns,alive_cells\n" + "".join(f"{i + 1},{c}\n" for i, c in enumerate(counts)))
+
+
 def cfg3():
     w = oracle.init_random(65536, 65536, seed=3)
     t = time.time()
@@ -42,11 +48,35 @@ def cfg3():
     d8 = oracle.digest_words(w)
     rest = oracle.packed_run_words(w, 992, threads=8)
     counts = np.concatenate([c8, rest])
-    return {"cfg3": {"width": 65536, "height": 65536, "seed": 3, "turns": 1000,
-                     "digest_after_8": d8, "digest_after_1000": oracle.digest_words(w),
+    d1000 = oracle.digest_words(w)
+    # every per-turn count up to 1200 (bench.py checks its alive_after_timed canary against these:
+    # the default run ends at turn 8 + 1000, the driver's at 5 + 20)
+    more = oracle.packed_run_words(w, 200, threads=8)
+    write_counts_csv("cfg3_65536_seed3_counts.csv", np.concatenate([counts, more]))
+    return {"cfg3": {"width": 65536, "height": 65536, "seed": 3, "turns": 1000, "csv_turns": 1200,
+                     "digest_after_8": d8, "digest_after_1000": d1000,
                      "counts_sha256": hashlib.sha256(counts.astype("<u8").tobytes()).hexdigest(),
+                     "counts_csv": "cfg3_65536_seed3_counts.csv",
                      "counts_every_50": {str(i + 1): int(counts[i]) for i in range(49, 1000, 50)},
                      "count_after_1": int(counts[0]), "oracle_seconds": round(time.time() - t, 1)}}
+
+
+def cfg4():
+    """configs[3]: 262144^2 random p=0.5 seed 4 (8 GiB packed; 2 x 8.6 GB of RAM).  Digests after
+    16 turns (the bench leg's warm-up launch) and 176 (+ its 160 timed turns) and every count."""
+    n = 262144
+    w = oracle.init_random(n, n, seed=4)
+    t = time.time()
+    c16 = oracle.packed_run_words(w, 16, threads=8)
+    d16 = oracle.digest_words(w)
+    rest = oracle.packed_run_words(w, 160, threads=8)
+    counts = np.concatenate([c16, rest])
+    write_counts_csv("cfg4_262144_seed4_counts.csv", counts)
+    return {"cfg4": {"width": n, "height": n, "seed": 4, "turns": 176,
+                     "digest_after_16": d16, "digest_after_176": oracle.digest_words(w),
+                     "counts_sha256": hashlib.sha256(counts.astype("<u8").tobytes()).hexdigest(),
+                     "counts_csv": "cfg4_262144_seed4_counts.csv",
+                     "oracle_seconds": round(time.time() - t, 1)}}
 
 
 def cfg5_board():
@@ -59,20 +89,32 @@ def cfg5_board():
 
 
 def cfg5():
+    """configs[4]: 4096^2 gun + R-pentomino, all 1e6 per-turn counts.  The counts are committed
+    as a delta-encoded, zlib-compressed int32 array (cfg5_4096_counts_1e6.npz) so tests compare
+    every tick with the golden count, not with the engine's own."""
     b = cfg5_board()
     w = oracle.pack(b)
     t = time.time()
     counts = oracle.packed_run_words(w, 100000, threads=8)
+    d100k = oracle.digest_words(w)
+    rest = oracle.packed_run_words(w, 900000, threads=8)
+    allc = np.concatenate([counts, rest])
+    deltas = np.diff(np.concatenate([[int((b == 255).sum())], allc])).astype("<i4")
+    np.savez_compressed(OUT / "cfg5_4096_counts_1e6.npz", deltas=deltas)
     return {"cfg5": {"width": 4096, "height": 4096, "turns": 100000,
                      "initial_alive": int((b == 255).sum()),
                      "counts_u32_sha256": hashlib.sha256(counts.astype("<u4").tobytes()).hexdigest(),
                      "counts_every_1000": {str(i + 1): int(counts[i]) for i in range(999, 100000, 1000)},
-                     "digest_after_100000": oracle.digest_words(w),
+                     "digest_after_100000": d100k,
+                     "turns_full": 1000000,
+                     "counts_1e6_u32_sha256": hashlib.sha256(allc.astype("<u4").tobytes()).hexdigest(),
+                     "counts_1e6_npz": "cfg5_4096_counts_1e6.npz",
+                     "digest_after_1000000": oracle.digest_words(w),
                      "oracle_seconds": round(time.time() - t, 1)}}
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["cfg2", "cfg3", "cfg5"]
+    which = sys.argv[1:] or ["cfg2", "cfg3", "cfg4", "cfg5"]
     path = OUT / "synthetic_golden.json"
     data = json.loads(path.read_text()) if path.exists() else {}
     for name in which:

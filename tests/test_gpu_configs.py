@@ -1,6 +1,6 @@
 """GPU parity at BASELINE.json's synthetic configs, against golden vectors the pinned oracle made
-(tests/golden/synthetic_golden.json, scripts/make_golden.py) and size-independent properties
-where the oracle cannot follow (262144^2)."""
+(tests/golden/synthetic_golden.json + the per-turn count files, scripts/make_golden.py): every
+engine result here is compared with the oracle's, never with another engine run."""
 import hashlib
 import json
 
@@ -26,54 +26,90 @@ def test_cfg2_5120_every_turn(golhip, oracle):
             assert oracle.digest_words(e.store_words()) == g["final_digest"]
 
 
-def test_cfg3_65536_thousand_turns(golhip, oracle):
-    """configs[2]: 65536^2 random (seed 3), 1000 turns: board digests and all 1000 counts."""
+CFG3_COUNTS = GOLDEN / "cfg3_65536_seed3_counts.csv"
+
+
+@pytest.mark.parametrize("k", [1, 2, 4, 8, 12, 16, 32])
+def test_cfg3_65536_thousand_turns(golhip, oracle, k):
+    """configs[2]: 65536^2 random (seed 3), 1000 turns at every launch depth -- the benchmarked
+    kernel (gol_stencil<16>, drifting sums, auto band grid) at the benchmarked size: board digests
+    after 8 and 1000 turns and all 1000 per-turn counts against the oracle's golden vectors."""
     g = GOLD["cfg3"]
-    with golhip.Engine(65536, 65536, k=8) as e:
+    with golhip.Engine(65536, 65536, k=k) as e:
         e.init_random(3)
         c8 = e.step(8, counts=True)
-        assert oracle.digest_words(e.store_words()) == g["digest_after_8"]
+        assert oracle.digest_words(e.store_words()) == g["digest_after_8"], k
         rest = e.step(992, counts=True)
-        assert oracle.digest_words(e.store_words()) == g["digest_after_1000"]
+        assert oracle.digest_words(e.store_words()) == g["digest_after_1000"], k
         counts = np.concatenate([c8, rest]).astype("<u8")
-        assert hashlib.sha256(counts.tobytes()).hexdigest() == g["counts_sha256"]
+        assert hashlib.sha256(counts.tobytes()).hexdigest() == g["counts_sha256"], k
         assert e.alive_count() == int(counts[-1])
 
 
-def test_cfg5_gun_and_r_pentomino(golhip, oracle):
-    """configs[4]: 4096^2 Gosper gun + R-pentomino; counts of the first 100000 turns."""
-    g = GOLD["cfg5"]
+@pytest.mark.parametrize("warmup,steps", [(5, 20), (8, 1000), (0, 17), (3, 45), (8, 1192)])
+def test_cfg3_bench_splits(golhip, oracle, warmup, steps):
+    """bench.py's own call pattern at k = 16 (warm-up call, then the timed call, each split into
+    launch depths by the engine's planner): the alive count after each call equals the oracle's
+    golden count of that turn (tests/golden/cfg3_65536_seed3_counts.csv)."""
+    expected = oracle.read_alive_csv(CFG3_COUNTS)
+    with golhip.Engine(65536, 65536, k=16) as e:
+        e.init_random(3)
+        if warmup:
+            e.step(warmup)
+            assert e.alive_count() == expected[warmup]
+        e.step(steps)
+        assert e.alive_count() == expected[warmup + steps]
+
+
+def cfg5_board(golhip):
     b = np.zeros((4096, 4096), dtype=np.uint8)
     golhip.place(b, golhip.parse_rle((GOLDEN / "gosper_gun.rle").read_text()), 64, 64)
     golhip.place(b, golhip.parse_rle((GOLDEN / "r_pentomino.rle").read_text()), 2048, 2048)
+    return b
+
+
+def cfg5_golden_counts():
+    """The oracle's count after each of the 1e6 turns (delta-encoded npz, scripts/make_golden.py)."""
+    g = GOLD["cfg5"]
+    d = np.load(GOLDEN / g["counts_1e6_npz"])["deltas"].astype(np.int64)
+    counts = g["initial_alive"] + np.cumsum(d)
+    assert hashlib.sha256(counts.astype("<u4").tobytes()).hexdigest() == g["counts_1e6_u32_sha256"]
+    return counts
+
+
+def test_cfg5_gun_and_r_pentomino(golhip, oracle):
+    """configs[4]: 4096^2 Gosper gun + R-pentomino, 1e6 turns: every per-turn count and the final
+    board against the oracle (SHA-256 of the uint32 count array of all 1e6 turns)."""
+    g = GOLD["cfg5"]
+    b = cfg5_board(golhip)
     assert int((b == 255).sum()) == g["initial_alive"]
+    golden = cfg5_golden_counts()
     with golhip.Engine(4096, 4096, k=16) as e:
         e.load(b)
-        counts = e.step(100000, counts=True)
-        assert hashlib.sha256(counts.astype("<u4").tobytes()).hexdigest() == g["counts_u32_sha256"]
+        first = e.step(100000, counts=True)
+        assert hashlib.sha256(first.astype("<u4").tobytes()).hexdigest() == g["counts_u32_sha256"]
         assert oracle.digest_words(e.store_words()) == g["digest_after_100000"]
+        rest = e.step(900000, counts=True)
+        counts = np.concatenate([first, rest]).astype(np.int64)
+        assert np.array_equal(counts, golden)
+        assert oracle.digest_words(e.store_words()) == g["digest_after_1000000"]
 
 
 @pytest.mark.parametrize("strips", [1, 2])
-def test_cfg4_262144_window_locality(golhip, oracle, strips):
-    """configs[3]: the 262144^2 board (8 GiB packed) is beyond the oracle, so check locality:
-    after t turns the cells of a window shrunk by t on every side depend only on the initial
-    window.  Windows straddle the torus wrap and (strips=2) the strip boundary."""
-    n, t = 262144, 24
-    with golhip.Engine(n, n, ngpus=1, k=8, strips=strips) as e:
+def test_cfg4_262144_against_oracle(golhip, oracle, strips):
+    """configs[3]: the 262144^2 board (seed 4, 8 GiB packed) on one GPU as 1 or 2 row strips (the
+    2-strip run exchanges halos across the seam): digests after 16 and 176 turns (the bench leg's
+    warm-up launch and its 160 timed turns) and all 176 per-turn counts against the oracle."""
+    g = GOLD["cfg4"]
+    n = 262144
+    with golhip.Engine(n, n, ngpus=1, k=16, strips=strips) as e:
         e.init_random(4)
-        counts = e.step(t, counts=True)
-        words = e.store_words()  # 8 GiB host copy: fine on the GPU box (>= 256 GiB host RAM)
-        # bottom 128 rows + top 128 rows (torus wrap) and rows around the middle (strip seam)
-        for y0 in (n - 128, n // 2 - 128):
-            rows = [(y0 + i) % n for i in range(256)]
-            init = np.concatenate([oracle.init_random(n, n, seed=4, y0=r, y1=r + 1) for r in rows])
-            win = init.copy()
-            # the window rows as their own torus: full width, so only the top/bottom t rows can
-            # differ from the real board
-            oracle.packed_run_words(win, t)
-            got = words[rows]
-            assert np.array_equal(got[t:-t], win[t:-t]), y0
+        c16 = e.step(16, counts=True)
+        assert oracle.digest_words(e.store_words()) == g["digest_after_16"]
+        rest = e.step(160, counts=True)
+        assert oracle.digest_words(e.store_words()) == g["digest_after_176"]
+        counts = np.concatenate([c16, rest]).astype("<u8")
+        assert hashlib.sha256(counts.tobytes()).hexdigest() == g["counts_sha256"]
         assert e.alive_count() == int(counts[-1])
 
 
@@ -91,13 +127,9 @@ def test_cfg5_host_run_ticker_and_keys(golhip, oracle, tmp_path):
 
     gol = ROOT / "distributed-gol_amd" / "lib" / "gol"
     assert gol.exists(), "host binary missing: run __graft_entry__.build()"
-    b = np.zeros((4096, 4096), dtype=np.uint8)
-    golhip.place(b, golhip.parse_rle((GOLDEN / "gosper_gun.rle").read_text()), 64, 64)
-    golhip.place(b, golhip.parse_rle((GOLDEN / "r_pentomino.rle").read_text()), 2048, 2048)
+    b = cfg5_board(golhip)
     turns = 1000000
-    with golhip.Engine(4096, 4096, k=16) as e:
-        e.load(b)
-        counts = [int(c) for c in e.step(turns, counts=True)]
+    counts = [int(c) for c in cfg5_golden_counts()]  # the oracle's, not the engine's
     initial = int((b == 255).sum())
 
     def count_after(t):
@@ -132,12 +164,16 @@ def test_cfg5_host_run_ticker_and_keys(golhip, oracle, tmp_path):
     assert len(snaps) == 1, states
     t_snap = int(snaps[0].rsplit("x", 1)[1])
     _, _, snap = oracle.read_pgm(out / (snaps[0] + ".pgm"))
+    # the paused snapshot is the board after its turn: its count is the golden count of that
+    # turn, and advanced to turn 1e6 it reaches the oracle's final board
+    assert int((snap == 255).sum()) == count_after(t_snap), t_snap
     with golhip.Engine(4096, 4096, k=16) as e:
-        e.load(b)
-        e.step(t_snap)
-        assert np.array_equal(snap, e.store()), t_snap
+        e.load(snap)
+        e.step(turns - t_snap)
+        assert oracle.digest_words(e.store_words()) == GOLD["cfg5"]["digest_after_1000000"], t_snap
     assert events[-1] == (turns, "Quitting"), events[-3:]
     final = re.search(r"Final turn (\d+): (\d+) alive cells", stdout)
     assert final and int(final.group(1)) == turns and int(final.group(2)) == counts[-1]
     _, _, last = oracle.read_pgm(out / ("4096x4096x%d.pgm" % turns))
     assert int((last == 255).sum()) == counts[-1]
+    assert oracle.digest_words(oracle.pack(last)) == GOLD["cfg5"]["digest_after_1000000"]

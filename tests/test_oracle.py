@@ -131,3 +131,43 @@ def test_synthetic_golden_vectors_are_the_oracle(oracle):
     counts = oracle.packed_run_words(w, 20)
     assert [int(c) for c in counts] == [expected[t] for t in range(1, 21)]
     assert set(gold) >= {"cfg2", "cfg3", "cfg5"}
+
+
+def test_golden_count_files_match_their_digests():
+    """The per-turn count files (cfg3 CSV, cfg4 CSV, cfg5 1e6 npz) hash to the SHA-256s recorded
+    beside them by scripts/make_golden.py, so GPU tests and bench.py compare against exactly the
+    oracle's counts."""
+    import json
+
+    from conftest import GOLDEN
+
+    gold = json.loads((GOLDEN / "synthetic_golden.json").read_text())
+    for cfg in ("cfg3", "cfg4"):
+        rows = (GOLDEN / gold[cfg]["counts_csv"]).read_text().splitlines()
+        assert rows[0] == "completed_turns,alive_cells"
+        n = gold[cfg].get("csv_turns", gold[cfg]["turns"])
+        counts = np.array([int(r.split(",")[1]) for r in rows[1:]], dtype="<u8")
+        assert [int(r.split(",")[0]) for r in rows[1:]] == list(range(1, n + 1))
+        counts = counts[: gold[cfg]["turns"]]
+        assert hashlib.sha256(counts.tobytes()).hexdigest() == gold[cfg]["counts_sha256"], cfg
+    g5 = gold["cfg5"]
+    d = np.load(GOLDEN / g5["counts_1e6_npz"])["deltas"].astype(np.int64)
+    c5 = g5["initial_alive"] + np.cumsum(d)
+    assert len(c5) == g5["turns_full"] == 1000000
+    assert hashlib.sha256(c5.astype("<u4").tobytes()).hexdigest() == g5["counts_1e6_u32_sha256"]
+    assert hashlib.sha256(c5[:100000].astype("<u4").tobytes()).hexdigest() == g5["counts_u32_sha256"]
+    assert all(int(c5[int(t) - 1]) == v for t, v in g5["counts_every_1000"].items())
+
+
+def test_cfg3_golden_prefix_is_the_oracle(oracle):
+    """First turns of configs[2] (65536^2, seed 3) recomputed on a 4096-row slab would differ
+    (torus), so recompute the real board for 2 turns (~1 s on 8 cores) against the count CSV."""
+    import json
+
+    from conftest import GOLDEN
+
+    gold = json.loads((GOLDEN / "synthetic_golden.json").read_text())
+    expected = oracle.read_alive_csv(GOLDEN / gold["cfg3"]["counts_csv"])
+    w = oracle.init_random(65536, 65536, seed=3)
+    counts = oracle.packed_run_words(w, 2)
+    assert [int(c) for c in counts] == [expected[1], expected[2]]
