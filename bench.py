@@ -222,6 +222,13 @@ def main():
 
     eng.step(a.warmup)
     eng.sync()
+    # the launch depths the engine runs for the timed region (golhip_launch_plan: the same planner
+    # golhip_step uses): k is the maximum depth, the bulk runs the fastest measured depth <= k
+    plan = golhip.launch_plan(width, height, a.k, a.steps, strips=world)
+    depth_count = {}
+    for d in plan:
+        depth_count[d] = depth_count.get(d, 0) + 1
+    dominant_k = max(depth_count, key=lambda d: (depth_count[d] * abs(d), d))
 
     # timed region: exactly a.steps generations, per-launch HIP events on the compute stream
     eng.timing(not a.no_timing)
@@ -253,14 +260,14 @@ def main():
     pmc_entry = {}
     try:
         pmc = json.loads(Path(a.pmc_file).read_text())
-        pmc_entry = pmc.get(f"{width}x{eng.info.rows}_k{a.k}", {})
+        pmc_entry = pmc.get(f"{width}x{eng.info.rows}_k{dominant_k}", {})
     except Exception:
         pass
     traffic = pmc_entry.get("hbm_bytes_per_launch")
-    uniform = launches > 0 and gens == launches * a.k  # every timed launch ran k generations
+    uniform = len(depth_count) == 1  # every timed launch ran the same depth
     issued = pmc_entry.get("valu_instr_per_launch")
-    kernel_name = "gol_step1" if a.k == 1 else f"gol_stencil<{a.k}>"
-    if a.k == 1:
+    kernel_name = "gol_step1" if dominant_k == 1 else f"gol_stencil<{dominant_k}>"
+    if dominant_k == 1:
         roof = {"bound": "hbm", "achieved": round(hbm_achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(hbm_achieved / HBM_PEAK_GBS, 4), "traffic": traffic}
     else:
@@ -277,7 +284,8 @@ def main():
         if pmc_entry.get("clock_ghz"):
             roof["clock_ghz_pmc"] = pmc_entry["clock_ghz"]
     roof.update({"kernel": kernel_name, "avg_launch_us": round(avg_launch_ms * 1e3, 2),
-                 "launches": launches, "gens_per_launch": round(gens_per_launch, 3)})
+                 "launches": launches, "gens_per_launch": round(gens_per_launch, 3),
+                 "launch_depths": {str(d): c for d, c in sorted(depth_count.items())}})
     hbm_roof = {"achieved": round(hbm_achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "algorithmic_over_peak": round(hbm_achieved / HBM_PEAK_GBS, 4),
                 "measured_traffic_per_launch": traffic,
@@ -295,7 +303,8 @@ def main():
     k1_launch_us = None
     if world == 1 and not a.no_sweep:
         sweep = {}
-        for kk in (1, 2, 4, 8, 12, 16, 32):
+        eng.set_fixed_k(True)  # exactly kk deep per launch
+        for kk in (1, 2, 4, 8, 10, 12, 14, 16, 32):
             eng.set_k(kk)
             # the first ~250 one-generation launches of a process run ~10 % slower (measured,
             # scripts/diag_k1.py), so k = 1 gets a longer untimed warmup
@@ -309,6 +318,7 @@ def main():
                 eng.timing(False)
             sweep[str(kk)] = round(width * height * n / t / 1e9, 1)
         eng.set_k(a.k)
+        eng.set_fixed_k(False)
 
     checksum = eng.alive_count()  # collective
     eng.close()
@@ -362,7 +372,8 @@ def main():
             "data": "synthetic (counter-based splitmix64 random board, p=0.5, generated on device)",
             "config": {
                 "workload": (f"{width}x{height} torus, random p=0.5 seed {a.seed}, "
-                             f"{world} row strip(s) of {local_rows} rows, k={a.k} gens/launch"),
+                             f"{world} row strip(s) of {local_rows} rows, up to k={a.k} gens/launch "
+                             f"(timed launches: " + " + ".join(f"{c}x{d}" for d, c in sorted(depth_count.items())) + ")"),
                 "width": width, "height": height, "k": a.k, "parallelism": f"rows{world}",
             },
             "parity": parity,

@@ -76,8 +76,9 @@ struct golhip_engine {
     int world_size = 1;
     int k = 1, halo = 0, band_rows = 0;
     int count_window = 4096;  // generations per count-window finalize
-    int variant = golhip::kVariantDriftLds;  // fastest measured (profiles/r01_tune_*)
+    int variant = golhip::kVariantProd;  // fastest measured per depth (golhip_internal.hpp)
     int cus = 0;                 // compute units of the first device (grid sizing)
+    bool fixed_k = false;        // golhip_set_fixed_k: long runs launch exactly k deep
     int waves_per_cu[golhip::kMaxK + 1][golhip::kNumVariants] = {};  // occupancy cache per (K, variant)
     bool rank_mode = false;
     bool split = false;  // board held as halo'd row strips (world > 1, or GOLHIP_RING_SELF)
@@ -226,14 +227,18 @@ int setup_engine(golhip_t h, int width, int height, int world, int k) {
                      : std::strcmp(e, "skewlds2") == 0 ? golhip::kVariantSkewLdsD2
                      : std::strcmp(e, "chainlds2") == 0 ? golhip::kVariantChainLdsD2
                      : std::strcmp(e, "chainlds") == 0 ? golhip::kVariantChainLdsPf
-                                                       : golhip::kVariantDriftLds;  // driftlds
+                     : std::strcmp(e, "driftzip") == 0 ? golhip::kVariantDriftZip
+                     : std::strcmp(e, "drift62") == 0 ? golhip::kVariantDrift62
+                     : std::strcmp(e, "driftnf") == 0 ? golhip::kVariantDriftNoFill
+                     : std::strcmp(e, "driftlds") == 0 ? golhip::kVariantDriftLds
+                                                       : golhip::kVariantProd;  // prod
     return GOLHIP_OK;
 }
 
 // Largest supported launch depth <= n.
 int pick_k(int n) {
     int kk = 1;
-    for (int c : {32, 16, 12, 8, 6, 4, 2, 1})
+    for (int c : {32, 16, 14, 12, 10, 8, 6, 4, 2, 1})
         if (c <= n && golhip::stencil_k_supported(c)) {
             kk = c;
             break;
@@ -241,22 +246,34 @@ int pick_k(int n) {
     return kk;
 }
 
-// Measured throughput of a K-generation launch, T cell-updates/s at 65536^2 (k sweep of
-// profiles/r01_bench.json: 1 -> 21.8, 2 -> 30.0, 4 -> 59.8, 32 -> 92.5; drift kernel at 8/12/16
-// from profiles/r01_tune_drift.txt; 6 interpolated), and the fixed cost of one launch (kernel
-// boundary + the last round's drain, us).
+// Measured throughput of a K-generation launch of the production variant, T cell-updates/s at
+// 65536^2: the mean of the two fixed-depth k sweeps of profiles/r02/bench_sweeps.json (one
+// process each; runs differ by up to 5 %, so depths 12-16 are a near tie and K = 16 keeps the
+// bulk; 6 interpolated), and the fixed cost of one launch (kernel boundary + the last round's
+// drain, us).
 double launch_rate_tcups(int K) {
     switch (K) {
-        case 1: return 21.8;
-        case 2: return 30.0;
-        case 4: return 59.8;
+        case 1: return 21.6;
+        case 2: return 33.8;
+        case 4: return 63.0;
         case 6: return 85.0;
-        case 8: return 109.4;
-        case 12: return 116.2;
-        case 16: return 118.9;
-        case 32: return 92.5;
+        case 8: return 106.4;
+        case 10: return 111.2;
+        case 12: return 114.9;
+        case 14: return 114.0;
+        case 16: return 117.9;
+        case 32: return 100.9;
         default: return 50.0;
     }
+}
+
+// The depth <= kmax with the highest measured rate: the bulk depth of long runs (k is the maximum
+// depth; deeper is not always faster -- 12 and 14 keep 5 waves per SIMD, 16 keeps 4).
+int best_rate_k(int kmax) {
+    int best = 1;
+    for (int K = 1; K <= kmax; ++K)
+        if (golhip::stencil_k_supported(K) && launch_rate_tcups(K) > launch_rate_tcups(best)) best = K;
+    return best;
 }
 constexpr double kLaunchOverheadUs = 4.0;
 
@@ -271,7 +288,7 @@ int plan_first_k(int64_t n, int kmax, double cells) {
     std::vector<int> first(N + 1, 1);
     best[0] = 0.0;
     for (int m = 1; m <= N; ++m)
-        for (int K : {32, 16, 12, 8, 6, 4, 2, 1}) {
+        for (int K : {32, 16, 14, 12, 10, 8, 6, 4, 2, 1}) {
             if (K > m || K > kmax || !golhip::stencil_k_supported(K)) continue;
             const double c = best[m - K] + cells * K / (launch_rate_tcups(K) * 1e6) + kLaunchOverheadUs;
             if (c < best[m]) {
@@ -301,8 +318,7 @@ int64_t auto_band(golhip_t h, int64_t rows_total, int K, int64_t reserve_waves =
     // The one-generation kernel (K = 1, production variant) is HBM-bound: it runs best with 2
     // long-streaming waves per SIMD in one round (measured: 2/SIMD 21.9, 4/SIMD 21.1, 1/SIMD
     // 19.6 TCUPS at 65536^2; uneven rounds lose 10-20 %, profiles/r01_tune_step1.txt).
-    const bool step1 = K == 1 && (h->variant == golhip::kVariantChainLdsPf ||
-                                  h->variant == golhip::kVariantDriftLds);
+    const bool step1 = K == 1 && golhip::variant_is_production_family(h->variant);
     const int64_t capacity = (int64_t)h->cus * (step1 ? golhip::kStep1WavesPerCu : wpc);
     constexpr int64_t kMaxBand = 4096;
     const bool skew = h->variant == golhip::kVariantSkew || h->variant == golhip::kVariantSkewD2 ||
@@ -365,7 +381,7 @@ int64_t auto_band(golhip_t h, int64_t rows_total, int K, int64_t reserve_waves =
 // when even minimal bands leave the chip short of waves (small boards, latency-bound), else 1.
 // GOLHIP_SPLIT=1/2/4/8 forces it (tests, tuning).
 int pick_split(golhip_t h, int64_t rows_total, int K) {
-    if (h->variant != golhip::kVariantChainLdsPf && h->variant != golhip::kVariantDriftLds) return 1;
+    if (!golhip::variant_is_production_family(h->variant)) return 1;
     if (h->force_split > 0)
         return h->force_split > 1 && golhip::stencil_split_supported(K, h->force_split)
                    ? h->force_split
@@ -402,7 +418,13 @@ int64_t max_band_rows(golhip_t h) {
 hipError_t launch_auto(golhip_t h, int K, const uint32_t *in, uint32_t *out,
                        const StencilParams &p, unsigned long long *slots, hipStream_t s) {
     const int S = pick_split(h, (p.r0e - p.r0b) + (p.r1e - p.r1b), K);
-    if (S > 1) return golhip::launch_stencil_split(K, S, in, out, p, slots, s);
+    if (S > 1) {
+        // the level-split kernel has its own column geometry (half-word halo for K <= 16)
+        StencilParams q = p;
+        const int per = golhip::split_chunk_words(K);
+        q.nchunks = (int32_t)((h->wd + per - 1) / per);
+        return golhip::launch_stencil_split(K, S, in, out, q, slots, s);
+    }
     return golhip::launch_stencil(K, h->variant, in, out, p, slots, s);
 }
 
@@ -708,6 +730,10 @@ int create_common(golhip_t h) {
     for (auto &s : h->shards) {
         int rc = alloc_shard(h, s);
         if (rc) return rc;
+        // each launch depth is its own code object, loaded at its first launch (~1 ms): load them
+        // all now, not inside the first timed or latency-sensitive step
+        HIPCHK(h, golhip::warm_stencils(h->variant, s.compute));
+        HIPCHK(h, hipStreamSynchronize(s.compute));
     }
     return GOLHIP_OK;
 }
@@ -715,11 +741,38 @@ int create_common(golhip_t h) {
 constexpr int kGraphGens = 128;  // generations per graph replay (<= count_window)
 
 // Graphs pay off when a launch is short (launch-bound): < ~100 us of stencil work.
+bool small_board(double cells, int K) { return cells * K <= 8e9; }
 bool graph_worthy(golhip_t h, int K) {
     if (h->split || h->shards.size() != 1) return false;
     if (const char *e = std::getenv("GOLHIP_GRAPHS")) return std::atoi(e) != 0;
-    return (double)h->L * (double)h->height * K <= 8e9;
+    return small_board((double)h->L * (double)h->height, K);
 }
+
+// The launch sequence of one golhip_step call (also exported as golhip_launch_plan): small boards
+// replay graphs of M launches of the deepest depth, then plan the tail; large boards run the
+// best-rate depth in bulk and plan the last < 2 bulk depths with plan_first_k.
+// next() returns 0 for one graph replay (M x Kfull generations), else one launch's depth.
+struct LaunchPlanner {
+    double cells;
+    int Kfull, Kbulk, M;
+    bool graphs;
+    int64_t left;
+    LaunchPlanner(double cells_, int k, int64_t turns, bool small, bool fixed = false)
+        : cells(cells_), Kfull(pick_k(k)), left(turns) {
+        M = std::max(2, (kGraphGens / Kfull) & ~1);
+        graphs = small && turns >= (int64_t)M * Kfull;
+        Kbulk = small || fixed ? Kfull : best_rate_k(Kfull);
+    }
+    int next() {
+        if (graphs && left >= (int64_t)M * Kfull) {
+            left -= (int64_t)M * Kfull;
+            return 0;
+        }
+        const int K = left >= 2 * (int64_t)Kbulk ? Kbulk : plan_first_k(left, Kfull, cells);
+        left -= K;
+        return K;
+    }
+};
 
 int graph_for(golhip_t h, int K, int M, bool counting, hipGraphExec_t *out) {
     Shard &s = h->shards[0];
@@ -1052,13 +1105,13 @@ int golhip_step(golhip_t h, int64_t turns, uint64_t *alive_per_turn) {
         if (rc) return rc;
     }
     int64_t done = 0;
-    const int Kfull = pick_k(h->k);
-    const int M = std::max(2, (kGraphGens / Kfull) & ~1);
-    const bool graphs = graph_worthy(h, Kfull) && turns >= (int64_t)M * Kfull;
+    LaunchPlanner plan((double)h->L * (double)h->height, h->k, turns, graph_worthy(h, pick_k(h->k)),
+                       h->fixed_k);
+    const int Kfull = plan.Kfull, M = plan.M;
     int64_t win = 0;  // generations pending in the count window, from turn offset done - win
     while (done < turns) {
-        const int64_t left = turns - done;
-        if (graphs && left >= (int64_t)M * Kfull) {
+        const int K = plan.next();
+        if (K == 0) {  // one graph replay of M x Kfull generations
             if (counting) {  // the graph finalizes its own generations from window slot 0
                 int rc = flush_counts_window(h, (int)win, done - win);
                 if (rc) return rc;
@@ -1082,9 +1135,6 @@ int golhip_step(golhip_t h, int64_t turns, uint64_t *alive_per_turn) {
             }
             continue;
         }
-        const int K = left >= 2 * (int64_t)Kfull
-                          ? Kfull
-                          : plan_first_k(left, Kfull, (double)h->L * (double)h->height);
         if (counting && win + K > h->count_window) {
             int rc = flush_counts_window(h, (int)win, done - win);
             if (rc) return rc;
@@ -1117,6 +1167,23 @@ int golhip_step(golhip_t h, int64_t turns, uint64_t *alive_per_turn) {
             for (int64_t i = 0; i < turns; ++i) alive_per_turn[i] /= rep;
     }
     return GOLHIP_OK;
+}
+
+int golhip_launch_plan(int64_t width, int64_t height, int strips, int k, int64_t turns,
+                       int32_t *depths, size_t cap, size_t *n) {
+    if (width <= 0 || height <= 0 || strips <= 0 || k < 1 || k > golhip::kMaxK || turns < 0 || !n)
+        return GOLHIP_ERR_ARG;
+    const double cells = (double)lcm64(width, 128) * (double)height;
+    const int Kfull = pick_k(k);
+    LaunchPlanner plan(cells, k, turns, strips == 1 && small_board(cells, Kfull));
+    size_t cnt = 0;
+    while (plan.left > 0) {
+        const int K = plan.next();
+        if (depths && cnt < cap) depths[cnt] = K == 0 ? -(plan.M * plan.Kfull) : K;
+        ++cnt;
+    }
+    *n = cnt;
+    return cnt > cap && depths ? GOLHIP_ERR_CAP : GOLHIP_OK;
 }
 
 int golhip_alive_count(golhip_t h, uint64_t *out) {
@@ -1169,6 +1236,12 @@ int golhip_set_k(golhip_t h, int k) {
         return fail(h, GOLHIP_ERR_ARG, "k=%d exceeds the %d halo rows allocated at create", k,
                     h->halo);
     h->k = k;
+    return GOLHIP_OK;
+}
+
+int golhip_set_fixed_k(golhip_t h, int fixed) {
+    if (!h) return GOLHIP_ERR_ARG;
+    h->fixed_k = fixed != 0;
     return GOLHIP_OK;
 }
 

@@ -43,7 +43,20 @@ constexpr int kVariantChainLdsPf = 5;
 constexpr int kVariantSkewLdsD2 = 6;   // LDS-DMA ring, 2 words (64 cells) per lane
 constexpr int kVariantChainLdsD2 = 7;
 constexpr int kVariantDriftLds = 8;    // chained LDS-DMA levels with drifting row sums (K <= 16)
-constexpr int kNumVariants = 9;
+constexpr int kVariantDriftZip = 9;    // drift, 62-word chunks, two steps interleaved (ZIP = 2)
+constexpr int kVariantDrift62 = 10;    // drift, 62-word chunks (one whole-word store per step)
+constexpr int kVariantDriftNoFill = 11;  // driftlds without the compile-time unrolled fill
+// Production: drifting sums at every depth, with the chunk geometry measured fastest per depth
+// (profiles/r02/tune_depth_geometry.txt, 65536^2): the half-word halo (63 words, 3 stores per
+// step) at K = 16, 62-word chunks (one store per step) at every other K >= 2; gol_step1 at K = 1.
+constexpr int kVariantProd = 12;
+constexpr int kNumVariants = 13;
+constexpr bool prod_half_halo(int K) { return K == 16; }
+// Variants of the production family: gol_step1 at K = 1, the level-split kernel for small boards.
+inline bool variant_is_production_family(int v) {
+    return v == kVariantChainLdsPf || v == kVariantDriftLds || v == kVariantDriftZip ||
+           v == kVariantDrift62 || v == kVariantDriftNoFill || v == kVariantProd;
+}
 inline int variant_words(int v) {
     return (v == kVariantSkewD2 || v == kVariantChainD2 || v == kVariantSkewLdsD2 ||
             v == kVariantChainLdsD2)
@@ -54,19 +67,22 @@ inline int variant_words(int v) {
 // words with the half-word halo (D = 1, K <= 16: lanes 0 and 63 own half a word each).
 constexpr int kStep1WavesPerCu = 8;  // gol_step1 grid: resident waves per CU it is sized for
 inline int chunk_words(int K, int variant) {
-    if (K == 1 && (variant == kVariantChainLdsPf || variant == kVariantDriftLds))
+    if (K == 1 && variant_is_production_family(variant))
         return 256;  // gol_step1: 4 words x 64 lanes
     const int d = variant_words(variant);
+    if (variant == kVariantDriftZip || variant == kVariantDrift62) return 62;
+    if (variant == kVariantProd) return prod_half_halo(K) ? 63 : 62;
     return (d == 1 && K <= 16) ? 63 : 62 * d;
 }
 
 // Launch depths with a stencil instantiation, one translation unit each (stencil_k<K>.hip).
-#define GOLHIP_STENCIL_DEPTHS(X) X(1) X(2) X(4) X(6) X(8) X(12) X(16) X(32)
+#define GOLHIP_STENCIL_DEPTHS(X) X(1) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(32)
 #define GOLHIP_X(K)                                                                           \
     hipError_t launch_stencil_k##K(int variant, const uint32_t *in, uint32_t *out,            \
                                    const StencilParams &p, unsigned long long *slots,        \
                                    hipStream_t s);                                           \
-    const void *stencil_fn_k##K(int variant);
+    const void *stencil_fn_k##K(int variant);                                                 \
+    hipError_t warm_stencil_k##K(int variant, hipStream_t s);
 GOLHIP_STENCIL_DEPTHS(GOLHIP_X)
 #undef GOLHIP_X
 
@@ -77,18 +93,24 @@ inline size_t lds_pad_bytes() {
     return e ? (size_t)std::atol(e) : (size_t)0;
 }
 
-// Launch the K-generation stencil (K in {1,2,4,6,8,12,16,32}). count_slots (nullable) receives
+// Launch the K-generation stencil (K in GOLHIP_STENCIL_DEPTHS). count_slots (nullable) receives
 // per-generation alive counts in kCountSlots slots per generation.
 hipError_t launch_stencil(int K, int variant, const uint32_t *in_row0, uint32_t *out_row0,
                           const StencilParams &p, unsigned long long *count_slots,
                           hipStream_t s);
 bool stencil_k_supported(int K);
+// Load every stencil code object (one per depth TU + the level-split TU) with empty launches, so
+// no code-object load lands inside a timed or latency-sensitive step.
+hipError_t warm_stencils(int variant, hipStream_t s);
+hipError_t warm_stencil_split(hipStream_t s);
 // Level-split stencil (small boards): the K levels of a (band, chunk) over a workgroup of S waves
 // (S = 2 or 4, D = 1, LDS-DMA input, chained levels; same geometry as kVariantChainLdsPf).
 hipError_t launch_stencil_split(int K, int S, const uint32_t *in_row0, uint32_t *out_row0,
                                 const StencilParams &p, unsigned long long *count_slots,
                                 hipStream_t s);
 bool stencil_split_supported(int K, int S);
+// Words per column chunk of the level-split kernel (half-word halo for K <= 16).
+__host__ __device__ constexpr int split_chunk_words(int K) { return K <= 16 ? 63 : 62; }
 // Resident waves per CU of the stencil launch (occupancy query), for sizing the grid.
 int stencil_waves_per_cu(int K, int variant);
 // Sum the slots of K generations into counts[0..K) and zero the slots.

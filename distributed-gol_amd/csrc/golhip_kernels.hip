@@ -268,7 +268,13 @@ inline unsigned grid_for(int64_t n, int threads = 256, int64_t cap = 8192) {
 }  // namespace
 
 bool stencil_k_supported(int K) {
-    return K == 1 || K == 2 || K == 4 || K == 6 || K == 8 || K == 12 || K == 16 || K == 32;
+    switch (K) {
+#define GOLHIP_X(KK) case KK:
+        GOLHIP_STENCIL_DEPTHS(GOLHIP_X)
+#undef GOLHIP_X
+        return true;
+        default: return false;
+    }
 }
 
 // The per-depth stencil launchers live in stencil_k<K>.hip (one TU per depth).
@@ -281,6 +287,16 @@ hipError_t launch_stencil(int K, int variant, const uint32_t *in_row0, uint32_t 
 #undef GOLHIP_X
         default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t warm_stencils(int variant, hipStream_t s) {
+    hipError_t e = hipSuccess;
+#define GOLHIP_X(KK) \
+    if (e == hipSuccess) e = warm_stencil_k##KK(variant, s);
+    GOLHIP_STENCIL_DEPTHS(GOLHIP_X)
+#undef GOLHIP_X
+    if (e == hipSuccess) e = warm_stencil_split(s);
+    return e;
 }
 
 int stencil_waves_per_cu(int K, int variant) {

@@ -1,0 +1,6 @@
+// stencil_k10.hip -- the 10-generation stencil launchers (every variant), one TU per launch depth.
+#include "golhip_stencil.hpp"
+
+namespace golhip {
+GOLHIP_DEFINE_STENCIL_K(10)
+}  // namespace golhip

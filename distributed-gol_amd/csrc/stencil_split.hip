@@ -23,4 +23,12 @@ hipError_t launch_stencil_split(int K, int S, const uint32_t *in_row0, uint32_t 
     return hipErrorInvalidValue;
 }
 
+hipError_t warm_stencil_split(hipStream_t s) {
+    StencilParams p{};
+    p.nchunks = 1;  // nbands = 0: the workgroup returns at once
+    hipLaunchKernelGGL((gol_stencil_split<16, false, 8>), dim3(1), dim3(64 * 8), 0, s, nullptr,
+                       nullptr, p, nullptr);
+    return hipGetLastError();
+}
+
 }  // namespace golhip

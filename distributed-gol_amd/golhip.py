@@ -39,7 +39,7 @@ EXPORTS = [
     "golhip_store_bytes", "golhip_store_words", "golhip_load_words", "golhip_step",
     "golhip_alive_count", "golhip_alive_cells", "golhip_flips", "golhip_turn",
     "golhip_set_turn", "golhip_set_k", "golhip_set_band_rows", "golhip_sync", "golhip_timing",
-    "golhip_kernel_time",
+    "golhip_kernel_time", "golhip_launch_plan", "golhip_set_fixed_k",
 ]
 
 
@@ -104,9 +104,12 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
         "golhip_set_turn": ([H, i64], i32),
         "golhip_set_k": ([H, i32], i32),
         "golhip_set_band_rows": ([H, i32], i32),
+        "golhip_set_fixed_k": ([H, i32], i32),
         "golhip_sync": ([H], i32),
         "golhip_timing": ([H, i32], i32),
         "golhip_kernel_time": ([H, ctypes.POINTER(ctypes.c_double), i64p, i64p], i32),
+        "golhip_launch_plan": ([i64, i64, i32, i32, i64, ctypes.c_void_p, ctypes.c_size_t,
+                                ctypes.POINTER(ctypes.c_size_t)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -175,6 +178,21 @@ def halo_plan(height: int, world_size: int, rank: int, k: int) -> list[tuple[str
     if rc != OK:
         raise GolHipError(rc, "halo_plan: invalid arguments")
     return [("send" if x.kind == 0 else "recv", x.peer, x.row, x.nrows) for x in arr]
+
+
+def launch_plan(width: int, height: int, k: int, turns: int, strips: int = 1) -> list[int]:
+    """The launch depths golhip_step(turns) runs (pure host arithmetic, no device): > 0 one
+    stencil launch of that depth, < 0 one graph replay of that many generations."""
+    L = load_library()
+    n = ctypes.c_size_t(0)
+    rc = L.golhip_launch_plan(width, height, strips, k, turns, None, 0, ctypes.byref(n))
+    if rc != OK:
+        raise GolHipError(rc, "launch_plan: invalid arguments")
+    out = np.zeros(max(n.value, 1), dtype=np.int32)
+    rc = L.golhip_launch_plan(width, height, strips, k, turns, out.ctypes.data, n.value, ctypes.byref(n))
+    if rc != OK:
+        raise GolHipError(rc, "launch_plan failed")
+    return [int(x) for x in out[: n.value]]
 
 
 def nccl_unique_id() -> bytes:
@@ -304,6 +322,10 @@ class Engine:
     def set_k(self, k: int):
         self._check(self._L.golhip_set_k(self._h, k))
         self.info = self.get_info()
+
+    def set_fixed_k(self, fixed: bool):
+        """Every bulk launch exactly k deep (depth sweeps); default: fastest measured depth <= k."""
+        self._check(self._L.golhip_set_fixed_k(self._h, int(fixed)))
 
     def set_band_rows(self, rows: int):
         self._check(self._L.golhip_set_band_rows(self._h, rows))

@@ -126,6 +126,15 @@ int golhip_load_words(golhip_t h, const uint64_t *in);
  * COLLECTIVE when alive_per_turn != NULL or world_size > 1.  Asynchronous when alive_per_turn
  * is NULL (use golhip_sync to wait). */
 int golhip_step(golhip_t h, int64_t turns, uint64_t *alive_per_turn);
+/* Pure host helper: the launch depths golhip_step(turns) runs on a width x height board held as
+ * `strips` row strips with maximum depth k (the reference has no such split: it runs one turn per
+ * Broker.Publish, gol/distributor.go:48-49).  depths[i] > 0: one stencil launch of that many
+ * generations; < 0: one captured graph replay of -depths[i] generations (small boards).  Large
+ * boards run the depth <= k with the highest measured rate in bulk and split the last ones by a
+ * modelled-time plan (e.g. 20 turns -> 10 + 10, not 16 + 4).  *n = number of entries; depths may
+ * be NULL to size the array; GOLHIP_ERR_CAP if cap is too small. */
+int golhip_launch_plan(int64_t width, int64_t height, int strips, int k, int64_t turns,
+                       int32_t *depths, size_t cap, size_t *n);
 /* Alive cells of the whole board (COLLECTIVE: sums over ranks). */
 int golhip_alive_count(golhip_t h, uint64_t *out);
 /* Alive cells of the handle's rows as (x, y) int32 pairs, row-major (gol/distributor.go:153-166).
@@ -140,6 +149,9 @@ int golhip_set_turn(golhip_t h, int64_t turn);
 
 /* ---- tuning / measurement ---------------------------------------------------------------- */
 int golhip_set_k(golhip_t h, int k);                 /* 1..32, <= halo_rows when world_size > 1 */
+/* k is the MAXIMUM launch depth: long runs use the depth <= k with the highest measured rate
+ * (golhip_launch_plan).  fixed != 0: every bulk launch is exactly k deep (depth sweeps). */
+int golhip_set_fixed_k(golhip_t h, int fixed);
 int golhip_set_band_rows(golhip_t h, int band_rows); /* 0 = automatic */
 int golhip_sync(golhip_t h);                         /* wait for all queued device work */
 /* HIP-event timing of golhip_step calls on the handle's first strip (one event pair per call

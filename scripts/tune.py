@@ -21,6 +21,7 @@ engines = {}
 for v in variants:
     os.environ["GOLHIP_VARIANT"] = v
     e = golhip.Engine(size, size, k=max(ks))
+    e.set_fixed_k(True)  # every launch exactly k deep
     e.init_random(3)
     engines[v] = e
 res = {}

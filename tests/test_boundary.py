@@ -69,3 +69,33 @@ def test_engine_without_device_fails_loudly(golhip):
         pytest.skip("a device is present")
     with pytest.raises(golhip.GolHipError):
         golhip.Engine(64, 64)
+
+
+SUPPORTED_DEPTHS = {1, 2, 4, 6, 8, 10, 12, 14, 16, 32}
+
+
+@pytest.mark.parametrize("turns", [1, 5, 17, 20, 25, 33, 45, 1000, 1192])
+def test_launch_plan_covers_the_turns(golhip, turns):
+    """golhip_launch_plan (the sequence golhip_step runs) advances exactly `turns` generations in
+    supported depths <= k, every launch depth the stencil is built for."""
+    plan = golhip.launch_plan(65536, 65536, 16, turns)
+    assert sum(plan) == turns
+    assert all(0 < d <= 16 and d in SUPPORTED_DEPTHS for d in plan)
+
+
+def test_launch_plan_short_runs_are_balanced(golhip):
+    """The driver's short run (20 turns) is split into two launches of near-equal depth, not the
+    greedy 16 + 4 (a 4-level launch runs at half the rate, profiles/r01_bench.json k sweep)."""
+    plan = golhip.launch_plan(65536, 65536, 16, 20)
+    assert len(plan) == 2 and min(plan) >= 8, plan
+    bulk = golhip.launch_plan(65536, 65536, 16, 1000)
+    assert len(bulk) <= 1000 // 10 + 2  # mostly deep launches
+
+
+def test_launch_plan_small_boards_replay_graphs(golhip):
+    """Small (launch-bound) boards replay captured graphs of deep launches (negative entries)."""
+    plan = golhip.launch_plan(4096, 4096, 16, 1000000)
+    graphs = [-d for d in plan if d < 0]
+    assert graphs and sum(graphs) + sum(d for d in plan if d > 0) == 1000000
+    assert not any(d < 0 for d in golhip.launch_plan(65536, 65536, 16, 1000))
+    assert not any(d < 0 for d in golhip.launch_plan(4096, 4096, 16, 1000000, strips=2))

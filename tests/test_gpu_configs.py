@@ -29,13 +29,14 @@ def test_cfg2_5120_every_turn(golhip, oracle):
 CFG3_COUNTS = GOLDEN / "cfg3_65536_seed3_counts.csv"
 
 
-@pytest.mark.parametrize("k", [1, 2, 4, 8, 12, 16, 32])
+@pytest.mark.parametrize("k", [1, 2, 4, 8, 10, 12, 14, 16, 32])
 def test_cfg3_65536_thousand_turns(golhip, oracle, k):
     """configs[2]: 65536^2 random (seed 3), 1000 turns at every launch depth -- the benchmarked
     kernel (gol_stencil<16>, drifting sums, auto band grid) at the benchmarked size: board digests
     after 8 and 1000 turns and all 1000 per-turn counts against the oracle's golden vectors."""
     g = GOLD["cfg3"]
     with golhip.Engine(65536, 65536, k=k) as e:
+        e.set_fixed_k(True)  # every bulk launch exactly k deep
         e.init_random(3)
         c8 = e.step(8, counts=True)
         assert oracle.digest_words(e.store_words()) == g["digest_after_8"], k

@@ -16,6 +16,7 @@ KS = [1, 2, 4, 8, 16, 32]
 def run_engine(golhip, board, turns, k=1, counts=False, band_rows=0):
     h, w = board.shape
     with golhip.Engine(w, h, k=k) as e:
+        e.set_fixed_k(True)  # launches exactly k deep (the planner would pick its fastest <= k)
         if band_rows:
             e.set_band_rows(band_rows)
         e.load(board)
@@ -208,7 +209,8 @@ def test_graph_replay_matches_launches(golhip, oracle, monkeypatch, k):
     assert len(cells) == int((exp == 255).sum())
 
 
-@pytest.mark.parametrize("variant", ["chainlds", "driftlds", "skewlds", "chainlds2", "skewlds2", "chain", "skew", "chain2", "skew2"])
+@pytest.mark.parametrize("variant", ["chainlds", "driftlds", "driftzip", "drift62", "driftnf", "skewlds", "chainlds2",
+                                     "skewlds2", "chain", "skew", "chain2", "skew2"])
 @pytest.mark.parametrize("k", [1, 6, 16])
 def test_every_kernel_variant(golhip, oracle, monkeypatch, variant, k):
     """Every stencil variant (chained/skewed levels, 1 or 2 words per lane, register or LDS-DMA
@@ -225,13 +227,16 @@ def test_every_kernel_variant(golhip, oracle, monkeypatch, variant, k):
             assert np.array_equal(counts.astype(np.int64), exp_counts), (variant, k, h, w, band)
 
 
-@pytest.mark.parametrize("k", [2, 4, 6, 8, 12, 16, 32])
-def test_drift_variant_every_k(golhip, oracle, monkeypatch, k):
-    """The drifting-sum stencil (rows move one bit east per level, one DPP per level update):
-    every launch depth, per-turn counts (per-level drifted ownership masks), multi-chunk rows
-    with a partial last chunk and widths that are not a multiple of 128 (replicated torus)."""
-    monkeypatch.setenv("GOLHIP_VARIANT", "driftlds")
-    for (h, w) in [(64, 4160), (35, 2016), (130, 8192), (9, 96)]:
+@pytest.mark.parametrize("variant", ["driftlds", "driftzip", "drift62"])
+@pytest.mark.parametrize("k", [2, 4, 6, 8, 10, 12, 14, 16, 32])
+def test_drift_variant_every_k(golhip, oracle, monkeypatch, variant, k):
+    """The drifting-sum stencils (rows move one bit east per level, one DPP per level update) --
+    half-word-halo chunks (driftlds), 62-word chunks (drift62) and 62-word chunks with two steps
+    interleaved (driftzip): every launch depth, per-turn counts (drifted count windows), multi-
+    chunk rows with a partial last chunk and widths that are not a multiple of 128 (replicated
+    torus)."""
+    monkeypatch.setenv("GOLHIP_VARIANT", variant)
+    for (h, w) in [(64, 4160), (35, 2016), (130, 8192), (9, 96), (20, 1984), (24, 3968)]:
         rng = np.random.default_rng(h * 31 + w + k)
         board = ((rng.random((h, w)) < 0.37) * 255).astype(np.uint8)
         turns = 3 * k + 5
