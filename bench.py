@@ -84,6 +84,7 @@ def parse():
     ap.add_argument("--pmc-file", default=str(ROOT / "profiles" / "pmc_traffic.json"))
     ap.add_argument("--no-strong", action="store_true",
                     help="skip the configs[3] leg (262144^2 board split over the N ranks)")
+    ap.add_argument("--no-flips", action="store_true", help="skip the per-turn CellFlipped leg")
     ap.add_argument("--strong-size", type=int, default=262144)
     ap.add_argument("--strong-steps", type=int, default=160)
     return ap.parse_args()
@@ -352,6 +353,35 @@ def main():
             strong["parity"] = {"turn": a.k + a.strong_steps, "golden": exp,
                                 "ok": int(strong_alive) == exp}
 
+    # per-turn CellFlipped path (gol/distributor.go:53-59; the TestSdl event stream): every turn's
+    # flips through golhip_step_flips (device ring + one extraction per call) vs the one-turn
+    # path (golhip_step(1) + golhip_flips per turn), wall time per turn incl. the host copy
+    flips = None
+    if world == 1 and not a.no_flips:
+        flips = {}
+        for n in (512, 5120):
+            fe = golhip.Engine(n, n, k=a.k)
+            fe.init_random(7)
+            cap = fe.flips_ring_capacity()
+            T = min(cap, 128)
+            fe.step_flips(T)  # allocate the ring, warm
+            reps = max(1, 2048 // T)
+            cells = 0
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                per_turn, _ = fe.step_flips(T)
+                cells += sum(len(x) for x in per_turn)
+            dt = time.perf_counter() - t0
+            t1 = time.perf_counter()
+            for _ in range(64):
+                fe.step(1)
+                fe.flips()
+            dt1 = time.perf_counter() - t1
+            fe.close()
+            flips[f"{n}x{n}"] = {"us_per_turn": round(dt / (reps * T) * 1e6, 2),
+                                 "turns_per_call": T, "flips_per_turn": round(cells / (reps * T), 1),
+                                 "us_per_turn_step1_then_flips": round(dt1 / 64 * 1e6, 2)}
+
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
         cpu = cpu_baseline(a.cpu_size, a.cpu_turns, threads_per_server=4)
@@ -391,6 +421,7 @@ def main():
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(BYTES_PER_CELL_UPDATE * local_cells / k1_launch_us / 1e3 / HBM_PEAK_GBS, 4)},
             "strong_262144": strong,
+            "flips_path": flips,
             "alive_after_timed": int(alive_timed),
             "alive_after": int(checksum),
         }

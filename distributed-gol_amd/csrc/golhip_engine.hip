@@ -52,6 +52,18 @@ struct Shard {
     unsigned long long *d_counts = nullptr;
     size_t d_counts_cap = 0;
     ncclComm_t comm_nccl = nullptr;
+    // flips (gol/distributor.go:53-59): the last generation's flips board (golhip_track_flips)
+    // and a ring of one flips board per turn (golhip_step_flips), rows x pitch words each
+    uint32_t *diffbuf = nullptr;
+    uint32_t *ring = nullptr;
+    // extraction scratch, allocated once (grown only for a larger ring / cell list): per-row
+    // counts, their exclusive scan, per-slot totals and the emitted (x, y) pairs
+    uint32_t *ex_rowcounts = nullptr;
+    unsigned long long *ex_offsets = nullptr;
+    unsigned long long *ex_slot_counts = nullptr;
+    int64_t ex_rows_cap = 0, ex_slots_cap = 0;
+    int32_t *ex_xy = nullptr;
+    size_t ex_xy_cap = 0;
 };
 
 struct TimingPair {
@@ -79,6 +91,10 @@ struct golhip_engine {
     int variant = golhip::kVariantProd;  // fastest measured per depth (golhip_internal.hpp)
     int cus = 0;                 // compute units of the first device (grid sizing)
     bool fixed_k = false;        // golhip_set_fixed_k: long runs launch exactly k deep
+    bool track_flips = false;    // golhip_track_flips: every step ends with a flips-writing launch
+    bool diff_valid = false;     // shards' diffbuf holds the flips of the last generation
+    int64_t ring_cap = 0;        // turns per golhip_step_flips call (flips ring slots)
+    int64_t ring_turns = 0;      // turns held in the ring by the last golhip_step_flips
     int waves_per_cu[golhip::kMaxK + 1][golhip::kNumVariants] = {};  // occupancy cache per (K, variant)
     bool rank_mode = false;
     bool split = false;  // board held as halo'd row strips (world > 1, or GOLHIP_RING_SELF)
@@ -154,6 +170,30 @@ int check_device_arch(golhip_t h, int device) {
     return GOLHIP_OK;
 }
 
+// Extraction scratch for `rows` rows (a tall board of `slots` slots for the flips ring): grown,
+// never shrunk -- a growth frees and reallocates, so it only happens for a larger ring.
+int ensure_extract_scratch(golhip_t h, Shard &s, int64_t rows, int64_t slots) {
+    if (rows <= s.ex_rows_cap && slots <= s.ex_slots_cap) return GOLHIP_OK;
+    HIPCHK(h, hipSetDevice(s.device));
+    HIPCHK(h, hipStreamSynchronize(s.compute));
+    if (rows > s.ex_rows_cap) {
+        if (s.ex_rowcounts) HIPCHK(h, hipFree(s.ex_rowcounts));
+        if (s.ex_offsets) HIPCHK(h, hipFree(s.ex_offsets));
+        s.ex_rowcounts = nullptr;
+        s.ex_offsets = nullptr;
+        HIPCHK(h, hipMalloc(&s.ex_rowcounts, sizeof(uint32_t) * (size_t)rows));
+        HIPCHK(h, hipMalloc(&s.ex_offsets, sizeof(unsigned long long) * (size_t)(rows + 1)));
+        s.ex_rows_cap = rows;
+    }
+    if (slots > s.ex_slots_cap) {
+        if (s.ex_slot_counts) HIPCHK(h, hipFree(s.ex_slot_counts));
+        s.ex_slot_counts = nullptr;
+        HIPCHK(h, hipMalloc(&s.ex_slot_counts, sizeof(unsigned long long) * (size_t)slots));
+        s.ex_slots_cap = slots;
+    }
+    return GOLHIP_OK;
+}
+
 int alloc_shard(golhip_t h, Shard &s) {
     HIPCHK(h, hipSetDevice(s.device));
     HIPCHK(h, hipStreamCreateWithFlags(&s.compute, hipStreamNonBlocking));
@@ -173,7 +213,7 @@ int alloc_shard(golhip_t h, Shard &s) {
                              s.compute));
     HIPCHK(h, hipMalloc(&s.scratch_u64, sizeof(unsigned long long) * 4));
     HIPCHK(h, hipStreamSynchronize(s.compute));
-    return GOLHIP_OK;
+    return ensure_extract_scratch(h, s, s.rows, 1);
 }
 
 void free_shard(Shard &s) {
@@ -187,6 +227,9 @@ void free_shard(Shard &s) {
     if (s.slots) (void)hipFree(s.slots);
     if (s.scratch_u64) (void)hipFree(s.scratch_u64);
     if (s.d_counts) (void)hipFree(s.d_counts);
+    for (void *q : {(void *)s.diffbuf, (void *)s.ring, (void *)s.ex_rowcounts, (void *)s.ex_offsets,
+                    (void *)s.ex_slot_counts, (void *)s.ex_xy})
+        if (q) (void)hipFree(q);
     if (s.ev_ready) (void)hipEventDestroy(s.ev_ready);
     if (s.ev_halo) (void)hipEventDestroy(s.ev_halo);
     if (s.ev_edge) (void)hipEventDestroy(s.ev_edge);
@@ -539,7 +582,10 @@ int exchange_halos(golhip_t h, int K) {
 
 // One K-generation block on every shard.  slot_gen >= 0: count the K generations into the count
 // window at generation slot_gen (finalized later by flush_counts_window), -1: no counts.
-int step_block(golhip_t h, int K, int64_t slot_gen) {
+// diff_slot: -1 no flips, kDiffLast the last generation's flips into diffbuf, t >= 0 into flips
+// ring slot t (the launch's last generation's flips are written beside its output).
+constexpr int64_t kDiffNone = -1, kDiffLast = -2;
+int step_block(golhip_t h, int K, int64_t slot_gen, int64_t diff_slot = kDiffNone) {
     if (h->split) {
         int rc = exchange_halos(h, K);
         if (rc) return rc;
@@ -551,8 +597,12 @@ int step_block(golhip_t h, int K, int64_t slot_gen) {
             slot_gen >= 0 ? s.slots + slot_gen * golhip::kCountSlots : nullptr;
         const uint32_t *in = h->row0(s, h->cur);
         uint32_t *out = h->row0(s, nxt);
+        uint32_t *diff = diff_slot == kDiffLast ? s.diffbuf
+                         : diff_slot >= 0      ? s.ring + diff_slot * s.rows * h->pitch
+                                               : nullptr;
         if (!h->split) {
             StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0);
+            p.diff = diff;
             HIPCHK(h, launch_auto(h, K, in, out, p, slots, s.compute));
         } else if (s.rows >= 3 * K) {
             // The interior rows need no halo: they run while the halos are exchanged.  The two
@@ -562,6 +612,7 @@ int step_block(golhip_t h, int K, int64_t slot_gen) {
             StencilParams pb = make_params(h, s, K, 0, K, s.rows - K, s.rows);
             const int64_t edge_waves = pb.nbands * (int64_t)pb.nchunks;
             StencilParams pi = make_params(h, s, K, K, s.rows - K, 0, 0, edge_waves);
+            pb.diff = pi.diff = diff;
             HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, pi, slots, s.compute));
             HIPCHK(h, hipStreamWaitEvent(s.edge, s.ev_halo, 0));
             HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, pb, slots, s.edge));
@@ -570,6 +621,7 @@ int step_block(golhip_t h, int K, int64_t slot_gen) {
         } else {
             HIPCHK(h, hipStreamWaitEvent(s.compute, s.ev_halo, 0));
             StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0);
+            p.diff = diff;
             HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, p, slots, s.compute));
         }
     }
@@ -580,6 +632,7 @@ int step_block(golhip_t h, int K, int64_t slot_gen) {
     h->cur = nxt;
     h->turn += K;
     h->prev_valid = (K == 1);
+    h->diff_valid = diff_slot == kDiffLast;
     return GOLHIP_OK;
 }
 
@@ -626,70 +679,82 @@ int reduce_u64(golhip_t h, const std::vector<unsigned long long *> &bufs, size_t
     return GOLHIP_OK;
 }
 
-// Extraction of cell lists (alive cells: b == nullptr; flips: b = previous generation).
-int extract(golhip_t h, bool flips, int32_t *xy, size_t cap, size_t *n) {
+// Cell lists, row-major (gol/distributor.go:153-166 alive cells, :53-59 flips): the set bits of
+// a[i] (XOR b[i] when b is given) in the first `width` columns of each shard's rows.  slots > 1:
+// a[i] is a tall board of `slots` consecutive boards of the shard's rows (the flips ring); the
+// list is then slot-major (turn by turn), per_slot[t] = cells of slot t (nullable).  The scratch
+// is preallocated; only a list longer than any before grows its output buffer.
+int extract_cells(golhip_t h, const std::vector<const uint32_t *> &a,
+                  const std::vector<const uint32_t *> &b, int64_t slots, int32_t *xy, size_t cap,
+                  size_t *n, uint64_t *per_slot) {
     if (!n) return fail(h, GOLHIP_ERR_ARG, "n is null");
-    if (flips && !h->prev_valid)
-        return fail(h, GOLHIP_ERR_STATE,
-                    "flips need the previous generation: step by 1 turn (k-blocked launches "
-                    "keep only the newest generation)");
-    size_t total = 0;
-    std::vector<unsigned long long> shard_totals(h->shards.size());
-    std::vector<std::pair<uint32_t *, unsigned long long *>> scratch(h->shards.size());
-    for (size_t i = 0; i < h->shards.size(); ++i) {
+    const size_t ns = h->shards.size();
+    std::vector<std::vector<unsigned long long>> cnt(ns, std::vector<unsigned long long>(slots));
+    for (size_t i = 0; i < ns; ++i) {
         Shard &s = h->shards[i];
+        const int64_t rows = s.rows * slots;
+        int rc = ensure_extract_scratch(h, s, rows, slots);
+        if (rc) return rc;
         HIPCHK(h, hipSetDevice(s.device));
-        uint32_t *rc = nullptr;
-        unsigned long long *off = nullptr;
-        HIPCHK(h, hipMalloc(&rc, sizeof(uint32_t) * (size_t)s.rows));
-        HIPCHK(h, hipMalloc(&off, sizeof(unsigned long long) * (size_t)(s.rows + 1)));
-        scratch[i] = {rc, off};
-        const uint32_t *a = h->row0(s, h->cur);
-        const uint32_t *b = flips ? h->row0(s, h->cur ^ 1) : nullptr;
-        HIPCHK(h, golhip::launch_extract_count(a, b, h->pitch, s.rows, h->width, rc, off,
-                                               s.compute));
-        HIPCHK(h, hipMemcpyAsync(&shard_totals[i], off + s.rows, sizeof(unsigned long long),
+        HIPCHK(h, golhip::launch_extract_count(a[i], b[i], h->pitch, rows, h->width,
+                                               s.ex_rowcounts, s.ex_offsets, s.compute));
+        HIPCHK(h, golhip::launch_extract_slot_counts(s.ex_offsets, s.rows, slots, s.ex_slot_counts,
+                                                     s.compute));
+        HIPCHK(h, hipMemcpyAsync(cnt[i].data(), s.ex_slot_counts,
+                                 sizeof(unsigned long long) * (size_t)slots,
                                  hipMemcpyDeviceToHost, s.compute));
     }
-    for (size_t i = 0; i < h->shards.size(); ++i) {
+    size_t total = 0;
+    std::vector<size_t> shard_total(ns, 0);
+    for (size_t i = 0; i < ns; ++i) {
         HIPCHK(h, hipSetDevice(h->shards[i].device));
         HIPCHK(h, hipStreamSynchronize(h->shards[i].compute));
-        total += shard_totals[i];
+        for (int64_t t = 0; t < slots; ++t) shard_total[i] += cnt[i][t];
+        total += shard_total[i];
     }
+    if (per_slot)
+        for (int64_t t = 0; t < slots; ++t) {
+            per_slot[t] = 0;
+            for (size_t i = 0; i < ns; ++i) per_slot[t] += cnt[i][t];
+        }
     *n = total;
-    int ret = GOLHIP_OK;
-    if (total > cap) {
-        ret = fail(h, GOLHIP_ERR_CAP, "%zu cells do not fit in cap %zu", total, cap);
-    } else if (total > 0) {
-        if (!xy) return fail(h, GOLHIP_ERR_ARG, "xy is null");
-        size_t base = 0;
-        for (size_t i = 0; i < h->shards.size(); ++i) {
-            Shard &s = h->shards[i];
-            const size_t cnt = shard_totals[i];
-            HIPCHK(h, hipSetDevice(s.device));
-            if (cnt) {
-                int32_t *dxy = nullptr;
-                HIPCHK(h, hipMalloc(&dxy, sizeof(int32_t) * 2 * cnt));
-                const uint32_t *a = h->row0(s, h->cur);
-                const uint32_t *b = flips ? h->row0(s, h->cur ^ 1) : nullptr;
-                HIPCHK(h, golhip::launch_extract_emit(a, b, h->pitch, s.rows, h->width,
-                                                      scratch[i].second, s.y0, dxy, cnt,
-                                                      s.compute));
-                HIPCHK(h, hipMemcpyAsync(xy + 2 * base, dxy, sizeof(int32_t) * 2 * cnt,
-                                         hipMemcpyDeviceToHost, s.compute));
-                HIPCHK(h, hipStreamSynchronize(s.compute));
-                HIPCHK(h, hipFree(dxy));
-            }
-            base += cnt;
+    if (total > cap) return fail(h, GOLHIP_ERR_CAP, "%zu cells do not fit in cap %zu", total, cap);
+    if (total == 0) return GOLHIP_OK;
+    if (!xy) return fail(h, GOLHIP_ERR_ARG, "xy is null");
+    // slot t of the output: the shards' cells of slot t in shard (row strip) order
+    std::vector<size_t> slot_base(slots + 1, 0);
+    for (int64_t t = 0; t < slots; ++t) {
+        slot_base[t + 1] = slot_base[t];
+        for (size_t i = 0; i < ns; ++i) slot_base[t + 1] += cnt[i][t];
+    }
+    for (size_t i = 0; i < ns; ++i) {
+        Shard &s = h->shards[i];
+        if (shard_total[i] == 0) continue;
+        HIPCHK(h, hipSetDevice(s.device));
+        if (shard_total[i] > s.ex_xy_cap) {  // grow the device list (rare: a longer list)
+            HIPCHK(h, hipStreamSynchronize(s.compute));
+            if (s.ex_xy) HIPCHK(h, hipFree(s.ex_xy));
+            s.ex_xy = nullptr;
+            const size_t want = std::max(shard_total[i], s.ex_xy_cap * 2);
+            HIPCHK(h, hipMalloc(&s.ex_xy, sizeof(int32_t) * 2 * want));
+            s.ex_xy_cap = want;
+        }
+        HIPCHK(h, golhip::launch_extract_emit(a[i], b[i], h->pitch, s.rows * slots, h->width,
+                                              s.ex_offsets, s.y0, s.rows, s.ex_xy,
+                                              shard_total[i], s.compute));
+        // the shard's list is slot-major; copy each slot's run to its place in the global list
+        size_t src = 0;
+        for (int64_t t = 0; t < slots; ++t) {
+            size_t dst = slot_base[t];
+            for (size_t i2 = 0; i2 < i; ++i2) dst += cnt[i2][t];
+            if (cnt[i][t])
+                HIPCHK(h, hipMemcpyAsync(xy + 2 * dst, s.ex_xy + 2 * src,
+                                         sizeof(int32_t) * 2 * cnt[i][t], hipMemcpyDeviceToHost,
+                                         s.compute));
+            src += cnt[i][t];
         }
     }
-    for (size_t i = 0; i < h->shards.size(); ++i) {
-        HIPCHK(h, hipSetDevice(h->shards[i].device));
-        HIPCHK(h, hipStreamSynchronize(h->shards[i].compute));
-        HIPCHK(h, hipFree(scratch[i].first));
-        HIPCHK(h, hipFree(scratch[i].second));
-    }
-    return ret;
+    return sync_all(h);
 }
 
 // Host <-> device byte transfer of the handle's rows, in row chunks of <= 64 MiB staging.
@@ -757,14 +822,16 @@ struct LaunchPlanner {
     int Kfull, Kbulk, M;
     bool graphs;
     int64_t left;
-    LaunchPlanner(double cells_, int k, int64_t turns, bool small, bool fixed = false)
-        : cells(cells_), Kfull(pick_k(k)), left(turns) {
+    bool keep_last;  // the last generation is always a plain launch (it writes the flips)
+    LaunchPlanner(double cells_, int k, int64_t turns, bool small, bool fixed = false,
+                  bool keep_last_ = false)
+        : cells(cells_), Kfull(pick_k(k)), left(turns), keep_last(keep_last_) {
         M = std::max(2, (kGraphGens / Kfull) & ~1);
-        graphs = small && turns >= (int64_t)M * Kfull;
+        graphs = small && turns >= (int64_t)M * Kfull + (keep_last ? 1 : 0);
         Kbulk = small || fixed ? Kfull : best_rate_k(Kfull);
     }
     int next() {
-        if (graphs && left >= (int64_t)M * Kfull) {
+        if (graphs && left >= (int64_t)M * Kfull + (keep_last ? 1 : 0)) {
             left -= (int64_t)M * Kfull;
             return 0;
         }
@@ -1011,6 +1078,7 @@ int golhip_load_bytes(golhip_t h, const uint8_t *cells, size_t row_stride) {
     if (rc) return rc;
     h->turn = 0;
     h->prev_valid = false;
+    h->diff_valid = false;
     return GOLHIP_OK;
 }
 
@@ -1031,6 +1099,7 @@ int golhip_init_random(golhip_t h, uint64_t seed, uint32_t density_q32) {
     }
     h->turn = 0;
     h->prev_valid = false;
+    h->diff_valid = false;
     return sync_all(h);
 }
 
@@ -1077,10 +1146,14 @@ int golhip_load_words(golhip_t h, const uint64_t *in) {
     }
     h->turn = 0;
     h->prev_valid = false;
+    h->diff_valid = false;
     return GOLHIP_OK;
 }
 
-int golhip_step(golhip_t h, int64_t turns, uint64_t *alive_per_turn) {
+// The body of golhip_step / golhip_step_flips.  ring: every generation is its own launch writing
+// its flips into ring slot t (t = 0 .. turns-1); otherwise the launch plan, and with flips
+// tracking on, the last launch writes the last generation's flips.
+static int run_steps(golhip_t h, int64_t turns, uint64_t *alive_per_turn, bool ring) {
     if (!h || turns < 0) return GOLHIP_ERR_ARG;
     if (turns == 0) return GOLHIP_OK;
     const bool counting = alive_per_turn != nullptr;
@@ -1105,8 +1178,8 @@ int golhip_step(golhip_t h, int64_t turns, uint64_t *alive_per_turn) {
         if (rc) return rc;
     }
     int64_t done = 0;
-    LaunchPlanner plan((double)h->L * (double)h->height, h->k, turns, graph_worthy(h, pick_k(h->k)),
-                       h->fixed_k);
+    LaunchPlanner plan((double)h->L * (double)h->height, ring ? 1 : h->k, turns,
+                       !ring && graph_worthy(h, pick_k(h->k)), h->fixed_k || ring, h->track_flips);
     const int Kfull = plan.Kfull, M = plan.M;
     int64_t win = 0;  // generations pending in the count window, from turn offset done - win
     while (done < turns) {
@@ -1129,6 +1202,7 @@ int golhip_step(golhip_t h, int64_t turns, uint64_t *alive_per_turn) {
             done += (int64_t)M * Kfull;
             h->turn += (int64_t)M * Kfull;
             h->prev_valid = (Kfull == 1);
+            h->diff_valid = false;
             if (h->timing) {
                 h->tlaunches += M;
                 h->tgens += (int64_t)M * Kfull;
@@ -1140,7 +1214,10 @@ int golhip_step(golhip_t h, int64_t turns, uint64_t *alive_per_turn) {
             if (rc) return rc;
             win = 0;
         }
-        int rc = step_block(h, K, counting ? win : -1);
+        const int64_t diff_slot = ring                                      ? done
+                                  : (h->track_flips && done + K == turns) ? kDiffLast
+                                                                          : kDiffNone;
+        int rc = step_block(h, K, counting ? win : -1, diff_slot);
         if (rc) return rc;
         done += K;
         if (counting) win += K;
@@ -1166,6 +1243,240 @@ int golhip_step(golhip_t h, int64_t turns, uint64_t *alive_per_turn) {
         if (rep > 1)
             for (int64_t i = 0; i < turns; ++i) alive_per_turn[i] /= rep;
     }
+    return GOLHIP_OK;
+}
+
+int golhip_step(golhip_t h, int64_t turns, uint64_t *alive_per_turn) {
+    return run_steps(h, turns, alive_per_turn, false);
+}
+
+// Ring slots per golhip_step_flips call: as many turns' flips boards as fit in ~1 GiB per strip
+// (5120^2: 319 turns; 512^2: 1024; 65536^2: 2).
+static int64_t ring_capacity(golhip_t h) {
+    int64_t rows = 1;
+    for (auto &s : h->shards) rows = std::max(rows, s.rows);
+    const int64_t board = rows * h->pitch * 4;
+    return std::max<int64_t>(1, std::min<int64_t>(1024, ((int64_t)1 << 30) / board));
+}
+
+int golhip_flips_ring_capacity(golhip_t h, int64_t *out) {
+    if (!h || !out) return GOLHIP_ERR_ARG;
+    *out = ring_capacity(h);
+    return GOLHIP_OK;
+}
+
+int golhip_step_flips(golhip_t h, int64_t turns, int32_t *xy, size_t cap, size_t *n,
+                      uint64_t *flips_per_turn, uint64_t *alive_per_turn) {
+    if (!h || turns < 0 || !n) return GOLHIP_ERR_ARG;
+    const int64_t rc_cap = ring_capacity(h);
+    if (turns > rc_cap)
+        return fail(h, GOLHIP_ERR_ARG, "%lld turns exceed the flips ring (%lld turns)",
+                    (long long)turns, (long long)rc_cap);
+    *n = 0;
+    if (turns == 0) return GOLHIP_OK;
+    if (h->ring_cap < rc_cap) {  // allocate the ring once per engine
+        for (auto &s : h->shards) {
+            HIPCHK(h, hipSetDevice(s.device));
+            HIPCHK(h, hipStreamSynchronize(s.compute));
+            if (s.ring) HIPCHK(h, hipFree(s.ring));
+            s.ring = nullptr;
+            HIPCHK(h, hipMalloc(&s.ring, sizeof(uint32_t) * (size_t)(rc_cap * s.rows * h->pitch)));
+            int rc = ensure_extract_scratch(h, s, rc_cap * s.rows, rc_cap);
+            if (rc) return rc;
+        }
+        h->ring_cap = rc_cap;
+    }
+    int rc = run_steps(h, turns, alive_per_turn, true);
+    if (rc) return rc;
+    h->ring_turns = turns;
+    std::vector<const uint32_t *> a, b(h->shards.size(), nullptr);
+    for (auto &s : h->shards) a.push_back(s.ring);
+    return extract_cells(h, a, b, turns, xy, cap, n, flips_per_turn);
+}
+
+int golhip_flips_fetch(golhip_t h, int32_t *xy, size_t cap, size_t *n, uint64_t *flips_per_turn) {
+    if (!h || !n) return GOLHIP_ERR_ARG;
+    if (h->ring_turns == 0)
+        return fail(h, GOLHIP_ERR_STATE, "no golhip_step_flips call holds flips in the ring");
+    int rc = sync_all(h);
+    if (rc) return rc;
+    std::vector<const uint32_t *> a, b(h->shards.size(), nullptr);
+    for (auto &s : h->shards) a.push_back(s.ring);
+    return extract_cells(h, a, b, h->ring_turns, xy, cap, n, flips_per_turn);
+}
+
+int golhip_track_flips(golhip_t h, int enable) {
+    if (!h) return GOLHIP_ERR_ARG;
+    h->track_flips = enable != 0;
+    if (h->track_flips)
+        for (auto &s : h->shards)
+            if (!s.diffbuf) {
+                HIPCHK(h, hipSetDevice(s.device));
+                HIPCHK(h, hipMalloc(&s.diffbuf, sizeof(uint32_t) * (size_t)(s.rows * h->pitch)));
+            }
+    return GOLHIP_OK;
+}
+
+// ---- checkpoint (the broker's paused worldSave/turn/size, broker/broker.go:124-155) ----------
+// File: a 64-byte little-endian header, then the handle's rows as packed bits, LSB-first
+// (bit b of byte i of a row is x = 8i + b; the bits past `width` in a row's last byte are 0).
+struct CkptHeader {
+    char magic[8];  // "GOLCKPT1"
+    uint32_t version, header_bytes;
+    int64_t width, height, y0, rows, turn;
+    uint64_t row_bytes;
+};
+static_assert(sizeof(CkptHeader) == 64, "checkpoint header layout");
+static const char kCkptMagic[8] = {'G', 'O', 'L', 'C', 'K', 'P', 'T', '1'};
+
+static int read_ckpt_header(FILE *f, CkptHeader *hd) {
+    if (std::fread(hd, sizeof *hd, 1, f) != 1) return GOLHIP_ERR_ARG;
+    if (std::memcmp(hd->magic, kCkptMagic, 8) != 0 || hd->version != 1 ||
+        hd->header_bytes != sizeof *hd || hd->width <= 0 || hd->height <= 0 || hd->rows <= 0 ||
+        hd->row_bytes != (uint64_t)((hd->width + 7) / 8) || hd->turn < 0)
+        return GOLHIP_ERR_ARG;
+    return GOLHIP_OK;
+}
+
+int golhip_checkpoint_info(const char *path, int64_t *width, int64_t *height, int64_t *turn) {
+    if (!path) return GOLHIP_ERR_ARG;
+    FILE *f = std::fopen(path, "rb");
+    if (!f) return GOLHIP_ERR_ARG;
+    CkptHeader hd;
+    const int rc = read_ckpt_header(f, &hd);
+    std::fclose(f);
+    if (rc) return rc;
+    if (width) *width = hd.width;
+    if (height) *height = hd.height;
+    if (turn) *turn = hd.turn;
+    return GOLHIP_OK;
+}
+
+// Rows [y, y + nr) of a shard <-> packed host rows (row_bytes each).  Widths that are a multiple
+// of 128 are the torus rows themselves (one 2-D copy); other widths go through the byte codec,
+// which also restores the horizontal replication of the torus on load.
+static int ckpt_rows(golhip_t h, Shard &s, int64_t y, int64_t nr, uint8_t *host, bool to_device) {
+    const int64_t W = h->width, rb = (W + 7) / 8;
+    uint32_t *dev = h->row0(s, h->cur) + y * h->pitch;
+    HIPCHK(h, hipSetDevice(s.device));
+    if (W % 128 == 0) {
+        if (to_device)
+            HIPCHK(h, hipMemcpy2DAsync(dev, (size_t)h->pitch * 4, host, (size_t)rb, (size_t)rb,
+                                       (size_t)nr, hipMemcpyHostToDevice, s.compute));
+        else
+            HIPCHK(h, hipMemcpy2DAsync(host, (size_t)rb, dev, (size_t)h->pitch * 4, (size_t)rb,
+                                       (size_t)nr, hipMemcpyDeviceToHost, s.compute));
+        HIPCHK(h, hipStreamSynchronize(s.compute));
+        return GOLHIP_OK;
+    }
+    std::vector<uint8_t> bytes((size_t)(nr * W));
+    uint8_t *stage = nullptr;
+    HIPCHK(h, hipMalloc(&stage, bytes.size()));
+    hipError_t e = hipSuccess;
+    if (to_device) {
+        for (int64_t r = 0; r < nr; ++r)
+            for (int64_t x = 0; x < W; ++x)
+                bytes[(size_t)(r * W + x)] = (host[r * rb + x / 8] >> (x % 8)) & 1 ? 255 : 0;
+        e = hipMemcpyAsync(stage, bytes.data(), bytes.size(), hipMemcpyHostToDevice, s.compute);
+        if (e == hipSuccess) e = golhip::launch_pack(stage, nr, W, h->wd, dev, h->pitch, s.compute);
+        if (e == hipSuccess) e = hipStreamSynchronize(s.compute);
+    } else {
+        e = golhip::launch_unpack(dev, h->pitch, nr, W, stage, s.compute);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(bytes.data(), stage, bytes.size(), hipMemcpyDeviceToHost, s.compute);
+        if (e == hipSuccess) e = hipStreamSynchronize(s.compute);
+        if (e == hipSuccess) {
+            std::memset(host, 0, (size_t)(nr * rb));
+            for (int64_t r = 0; r < nr; ++r)
+                for (int64_t x = 0; x < W; ++x)
+                    if (bytes[(size_t)(r * W + x)]) host[r * rb + x / 8] |= (uint8_t)(1u << (x % 8));
+        }
+    }
+    (void)hipFree(stage);
+    HIPCHK(h, e);
+    return GOLHIP_OK;
+}
+
+int golhip_checkpoint_save(golhip_t h, const char *path) {
+    if (!h || !path) return GOLHIP_ERR_ARG;
+    int rc = sync_all(h);
+    if (rc) return rc;
+    const std::string tmp = std::string(path) + ".tmp";
+    FILE *f = std::fopen(tmp.c_str(), "wb");
+    if (!f) return fail(h, GOLHIP_ERR_ARG, "cannot write %s", tmp.c_str());
+    CkptHeader hd{};
+    std::memcpy(hd.magic, kCkptMagic, 8);
+    hd.version = 1;
+    hd.header_bytes = sizeof hd;
+    hd.width = h->width;
+    hd.height = h->height;
+    hd.y0 = h->shards.front().y0;
+    hd.rows = 0;
+    for (auto &s : h->shards) hd.rows += s.rows;
+    hd.turn = h->turn;
+    hd.row_bytes = (uint64_t)((h->width + 7) / 8);
+    bool ok = std::fwrite(&hd, sizeof hd, 1, f) == 1;
+    const int64_t chunk = std::max<int64_t>(1, (64ll << 20) / (int64_t)hd.row_bytes);
+    std::vector<uint8_t> buf;
+    for (auto &s : h->shards)
+        for (int64_t y = 0; ok && y < s.rows; y += chunk) {
+            const int64_t nr = std::min(chunk, s.rows - y);
+            buf.resize((size_t)(nr * (int64_t)hd.row_bytes));
+            if ((rc = ckpt_rows(h, s, y, nr, buf.data(), false))) break;
+            ok = std::fwrite(buf.data(), 1, buf.size(), f) == buf.size();
+        }
+    ok = (std::fclose(f) == 0) && ok;
+    if (rc || !ok) {
+        std::remove(tmp.c_str());
+        return rc ? rc : fail(h, GOLHIP_ERR_ARG, "short write to %s", tmp.c_str());
+    }
+    if (std::rename(tmp.c_str(), path) != 0) {  // atomic replace: never a half-written checkpoint
+        std::remove(tmp.c_str());
+        return fail(h, GOLHIP_ERR_ARG, "cannot rename %s to %s", tmp.c_str(), path);
+    }
+    return GOLHIP_OK;
+}
+
+int golhip_checkpoint_load(golhip_t h, const char *path) {
+    if (!h || !path) return GOLHIP_ERR_ARG;
+    int rc = sync_all(h);
+    if (rc) return rc;
+    FILE *f = std::fopen(path, "rb");
+    if (!f) return fail(h, GOLHIP_ERR_ARG, "cannot read %s", path);
+    CkptHeader hd;
+    if ((rc = read_ckpt_header(f, &hd))) {
+        std::fclose(f);
+        return fail(h, rc, "%s is not a golhip checkpoint", path);
+    }
+    int64_t rows = 0;
+    for (auto &s : h->shards) rows += s.rows;
+    if (hd.width != h->width || hd.height != h->height || hd.y0 != h->shards.front().y0 ||
+        hd.rows != rows) {
+        std::fclose(f);
+        return fail(h, GOLHIP_ERR_STATE,
+                    "checkpoint holds rows [%lld, %lld) of a %lldx%lld board, this handle rows "
+                    "[%lld, %lld) of %lldx%lld",
+                    (long long)hd.y0, (long long)(hd.y0 + hd.rows), (long long)hd.width,
+                    (long long)hd.height, (long long)h->shards.front().y0,
+                    (long long)(h->shards.front().y0 + rows), (long long)h->width,
+                    (long long)h->height);
+    }
+    const int64_t chunk = std::max<int64_t>(1, (64ll << 20) / (int64_t)hd.row_bytes);
+    std::vector<uint8_t> buf;
+    bool ok = true;
+    for (auto &s : h->shards)
+        for (int64_t y = 0; ok && y < s.rows; y += chunk) {
+            const int64_t nr = std::min(chunk, s.rows - y);
+            buf.resize((size_t)(nr * (int64_t)hd.row_bytes));
+            ok = std::fread(buf.data(), 1, buf.size(), f) == buf.size();
+            if (ok && (rc = ckpt_rows(h, s, y, nr, buf.data(), true))) break;
+        }
+    std::fclose(f);
+    if (rc) return rc;
+    if (!ok) return fail(h, GOLHIP_ERR_ARG, "%s is truncated", path);
+    h->turn = hd.turn;
+    h->prev_valid = false;
+    h->diff_valid = false;
     return GOLHIP_OK;
 }
 
@@ -1207,14 +1518,31 @@ int golhip_alive_cells(golhip_t h, int32_t *xy, size_t cap, size_t *n) {
     if (!h) return GOLHIP_ERR_ARG;
     int rc = sync_all(h);
     if (rc) return rc;
-    return extract(h, false, xy, cap, n);
+    std::vector<const uint32_t *> a, b(h->shards.size(), nullptr);
+    for (auto &s : h->shards) a.push_back(h->row0(s, h->cur));
+    return extract_cells(h, a, b, 1, xy, cap, n, nullptr);
 }
 
 int golhip_flips(golhip_t h, int32_t *xy, size_t cap, size_t *n) {
     if (!h) return GOLHIP_ERR_ARG;
     int rc = sync_all(h);
     if (rc) return rc;
-    return extract(h, true, xy, cap, n);
+    std::vector<const uint32_t *> a, b(h->shards.size(), nullptr);
+    if (h->diff_valid) {  // written by the last launch beside its output
+        for (auto &s : h->shards) a.push_back(s.diffbuf);
+    } else if (h->prev_valid) {  // a one-generation launch: XOR with the buffer it read
+        b.clear();
+        for (auto &s : h->shards) {
+            a.push_back(h->row0(s, h->cur));
+            b.push_back(h->row0(s, h->cur ^ 1));
+        }
+    } else {
+        if (n) *n = 0;
+        return fail(h, GOLHIP_ERR_STATE,
+                    "flips of the last generation are not held: enable golhip_track_flips (or "
+                    "step by 1 turn) before stepping");
+    }
+    return extract_cells(h, a, b, 1, xy, cap, n, nullptr);
 }
 
 int golhip_turn(golhip_t h, int64_t *out) {

@@ -27,6 +27,10 @@ struct StencilParams {
     int64_t lo, hi;      // halo mode: readable input rows [lo, hi) relative to row 0
     int32_t wd;          // words per row of the torus
     int32_t nchunks;     // column chunks per row (chunk_words() words each)
+    // nullable: row 0 of a board (same pitch and rows) that receives the XOR of the output
+    // generation with the one before it -- the cells the launch's last generation flipped
+    // (gol/distributor.go:53-59), written beside the output rows (no extra pass)
+    uint32_t *diff;
 };
 
 constexpr int kMaxK = 32;         // generations per launch limit (halo lane = 32 bits)
@@ -135,9 +139,14 @@ hipError_t launch_popcount(const uint32_t *row0, int64_t pitch, int64_t rows, in
 hipError_t launch_extract_count(const uint32_t *a, const uint32_t *b, int64_t pitch,
                                 int64_t rows, int64_t width, uint32_t *row_counts,
                                 unsigned long long *offsets, hipStream_t s);
+// slot_rows: rows per slot of a tall board of slots (y is reported within its slot).
 hipError_t launch_extract_emit(const uint32_t *a, const uint32_t *b, int64_t pitch,
                                int64_t rows, int64_t width, const unsigned long long *offsets,
-                               int64_t gy0, int32_t *xy, uint64_t cap, hipStream_t s);
+                               int64_t gy0, int64_t slot_rows, int32_t *xy, uint64_t cap,
+                               hipStream_t s);
+// counts[t] = cells of slot t (rows [t * slot_rows, (t+1) * slot_rows)) from the extract scan.
+hipError_t launch_extract_slot_counts(const unsigned long long *offsets, int64_t slot_rows,
+                                      int64_t slots, unsigned long long *counts, hipStream_t s);
 // Packed torus rows <-> logical uint64 words (width % 64 == 0; first width bits of each row).
 hipError_t launch_words_out(const uint32_t *row0, int64_t pitch, int64_t rows, int64_t width,
                             uint64_t *words, hipStream_t s);

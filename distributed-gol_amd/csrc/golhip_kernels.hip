@@ -200,10 +200,21 @@ __global__ void extract_scan(const uint32_t *__restrict__ row_counts, int64_t ro
     }
 }
 
+// Cells of slot t = rows [t * slot_rows, (t+1) * slot_rows) of a tall board: counts[t].
+__global__ void extract_slot_counts(const unsigned long long *__restrict__ offsets,
+                                    int64_t slot_rows, int64_t slots,
+                                    unsigned long long *__restrict__ counts) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < slots;
+         t += (int64_t)gridDim.x * blockDim.x)
+        counts[t] = offsets[(t + 1) * slot_rows] - offsets[t * slot_rows];
+}
+
+// (x, y) of every cell, row-major; a tall board of slots reports y within its slot
+// (y = gy0 + row % slot_rows), slot-major.
 __global__ void extract_emit(const uint32_t *__restrict__ a, const uint32_t *__restrict__ b,
                              int64_t pitch, int64_t rows, int32_t nw, uint32_t lastmask,
                              const unsigned long long *__restrict__ offsets, int64_t gy0,
-                             int32_t *__restrict__ xy, uint64_t cap) {
+                             int64_t slot_rows, int32_t *__restrict__ xy, uint64_t cap) {
     const int lane = threadIdx.x & 63;
     const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
     for (int64_t y = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); y < rows;
@@ -226,7 +237,7 @@ __global__ void extract_emit(const uint32_t *__restrict__ a, const uint32_t *__r
                 v &= v - 1;
                 if (pos < cap) {
                     xy[2 * pos] = col * 32 + bit;
-                    xy[2 * pos + 1] = (int32_t)(gy0 + y);
+                    xy[2 * pos + 1] = (int32_t)(gy0 + y % slot_rows);
                 }
                 ++pos;
             }
@@ -373,13 +384,21 @@ hipError_t launch_extract_count(const uint32_t *a, const uint32_t *b, int64_t pi
 
 hipError_t launch_extract_emit(const uint32_t *a, const uint32_t *b, int64_t pitch,
                                int64_t rows, int64_t width, const unsigned long long *offsets,
-                               int64_t gy0, int32_t *xy, uint64_t cap, hipStream_t s) {
+                               int64_t gy0, int64_t slot_rows, int32_t *xy, uint64_t cap,
+                               hipStream_t s) {
     int32_t nw;
     uint32_t lastmask;
     extract_geometry(width, nw, lastmask);
     const unsigned blocks = grid_for(rows * 64, 256, 16384);
     hipLaunchKernelGGL(extract_emit, dim3(blocks), dim3(256), 0, s, a, b, pitch, rows, nw,
-                       lastmask, offsets, gy0, xy, cap);
+                       lastmask, offsets, gy0, slot_rows, xy, cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_extract_slot_counts(const unsigned long long *offsets, int64_t slot_rows,
+                                      int64_t slots, unsigned long long *counts, hipStream_t s) {
+    hipLaunchKernelGGL(extract_slot_counts, dim3(grid_for(slots, 256, 64)), dim3(256), 0, s,
+                       offsets, slot_rows, slots, counts);
     return hipGetLastError();
 }
 

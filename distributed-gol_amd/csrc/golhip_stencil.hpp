@@ -329,8 +329,12 @@ __device__ __forceinline__ void flush_counts(const uint32_t (&acc)[NL], int j0, 
 //             it, with an s_nop before every DPP), at the cost of a second chain's temporaries.
 // FILLU = false: the pipeline-fill steps run through the steady loop (garbage levels computed and
 //             dropped) instead of being unrolled at compile time -- a smaller code footprint.
+// LD = true: also store the last generation's flips (output XOR the generation before it) to
+//             p.diff: at the last level the mid row's centre cells are generation K-1 in the same
+//             (drifted) frame as the output, so the diff costs one XOR, its realignment and the
+//             store(s) per step.
 template <int K, bool COUNT, bool SKEW, int D, int PF, bool HH, bool DR = false, int ZIP = 1,
-          bool FILLU = true>
+          bool FILLU = true, bool LD = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZIP == 2 && !COUNT && K >= 12 && K <= 16 ? 4 : 1)))
 void gol_stencil(const uint32_t *__restrict__ in,
                                                    uint32_t *__restrict__ out, StencilParams p,
@@ -375,8 +379,24 @@ void gol_stencil(const uint32_t *__restrict__ in,
     // the last chunk's window ends at cell 32 wd + 32 - d, i.e. at the lane with colraw == wd (the
     // wrapped word 0, whose cells [0, 32 - d) no chunk's first window covers).
     const bool count_lane = HH ? (lane >= 1 && colraw < p.wd) : (lane >= 2 && colraw <= p.wd);
-    constexpr int NSTORE = HH ? 3 : 1;  // vector-memory stores per step
-    auto store_row = [&](const Words<D> &v, int rowoff) { golhip::store_row<D, HH>(orsrc, ls, v, rowoff); };
+    // vector-memory stores per step: the output row (3 with the half-word halo), twice with LD
+    constexpr int NSTORE = (HH ? 3 : 1) * (LD ? 2 : 1);
+    __amdgpu_buffer_rsrc_t drsrc = orsrc;
+    if constexpr (LD)
+        drsrc = __builtin_amdgcn_make_buffer_rsrc(p.diff + (int64_t)ya * p.pitch, 0,
+                                                  (yb - ya) * rowbytes, kBufferRsrcWord3);
+    // the output row (and, LD, its diff): rowoff kOutOfRange (+ small offsets) drops the stores
+    auto store_row = [&](const Words<D> &v, int rowoff, const Words<D> *dv = nullptr) {
+        golhip::store_row<D, HH>(orsrc, ls, v, rowoff);
+        if constexpr (LD) golhip::store_row<D, HH>(drsrc, ls, dv ? *dv : v, rowoff);
+    };
+    // the diff of the last level's output nx against its mid row's centre cells (same frame)
+    auto last_diff = [&](const Words<D> &nx, const RowState<D> &mid) {
+        Words<D> dv;
+#pragma unroll
+        for (int d = 0; d < D; ++d) dv.w[d] = nx.w[d] ^ mid.c.w[d];
+        return dv;
+    };
 
     // Per level: a two-slot ring (X/Y swap roles every step) and, skewed, the pending input row.
     RowState<D> X[K], Y[K];
@@ -429,6 +449,8 @@ void gol_stencil(const uint32_t *__restrict__ in,
                 level_update<D, DR>(PAR == 0 ? X[j] : Y[j], PAR == 0 ? Y[j] : X[j], lin, nx, nb0);
             else
                 level_update<D, DR>(PAR == 0 ? X[j] : Y[j], PAR == 0 ? Y[j] : X[j], lin, nx);
+            Words<D> dv{};
+            if (LD && j == K - 1) dv = last_diff(nx, PAR == 0 ? Y[j] : X[j]);
             if (COUNT) {
                 const int r = SKEW ? st - K - 1 - 2 * j : st - K - (j + 1);
                 const uint32_t m = DR ? ~0u : own_mask;  // DR: whole words, see count_lane
@@ -437,9 +459,11 @@ void gol_stencil(const uint32_t *__restrict__ in,
             }
             if (j == K - 1) {
                 const int r = st - lag;  // stored row - ya
-                if constexpr (DR)  // back to the board frame: K bits west
+                if constexpr (DR) {  // back to the board frame: K bits west
                     nx.w[0] = realign_drift<K>(nx.w[0]);
-                store_row(nx, (r >= 0 && r < nrows) ? r * rowbytes : kOutOfRange);
+                    if constexpr (LD) dv.w[0] = realign_drift<K>(dv.w[0]);
+                }
+                store_row(nx, (r >= 0 && r < nrows) ? r * rowbytes : kOutOfRange, &dv);
                 if (PF) asm volatile("" ::: "memory");
             } else if (SKEW) {
                 pend[j + 1] = nx;
@@ -477,6 +501,8 @@ void gol_stencil(const uint32_t *__restrict__ in,
                 level_update<D, DR>(above, mid, nc, nx, nb0);
             else
                 level_update<D, DR>(above, mid, nc, nx);
+            Words<D> dv{};
+            if constexpr (LD && j == K - 1) dv = last_diff(nx, mid);
             if (COUNT) {
                 const int r = st - K - (j + 1);
                 const uint32_t m = DR ? ~0u : own_mask;  // DR: whole words, see count_lane
@@ -484,9 +510,11 @@ void gol_stencil(const uint32_t *__restrict__ in,
             }
             if constexpr (j == K - 1) {
                 const int r = st - lag;
-                if constexpr (DR)
+                if constexpr (DR) {
                     nx.w[0] = realign_drift<K>(nx.w[0]);
-                store_row(nx, (r >= 0 && r < nrows) ? r * rowbytes : kOutOfRange);
+                    if constexpr (LD) dv.w[0] = realign_drift<K>(dv.w[0]);
+                }
+                store_row(nx, (r >= 0 && r < nrows) ? r * rowbytes : kOutOfRange, &dv);
                 asm volatile("" ::: "memory");
             }
             nc = nx;
@@ -532,7 +560,7 @@ void gol_stencil(const uint32_t *__restrict__ in,
         // (D + NSTORE) ops for each of the PL-2 steps after it; the wait leaves a margin of 2.
         // Deeper ring for K <= 2: steps are short, the launch is HBM-bound and needs more bytes
         // in flight per CU.
-        constexpr int PL = K <= 2 ? 16 : 8;
+        constexpr int PL = (K <= 2 && NSTORE + (D + NSTORE) * 14 - 2 <= 63) ? 16 : 8;
         constexpr int kWait = NSTORE + (D + NSTORE) * (PL - 2) - 2;
         static_assert(kWait <= 63, "vmcnt field");
         __shared__ __attribute__((aligned(16))) uint32_t ring[4][PL][64 * D];
@@ -669,7 +697,7 @@ void gol_stencil(const uint32_t *__restrict__ in,
 // wrapped words (the torus continuation), so partial last chunks need no special case; they
 // just do not store.
 // P = rows in flight per wave; NT bit 0 / bit 1 = non-temporal loads / stores (streamed once).
-template <bool COUNT, int P = 8, int NT = 0>
+template <bool COUNT, int P = 8, int NT = 0, bool LD = false>
 __global__ __launch_bounds__(256) void gol_step1(const uint32_t *__restrict__ in,
                                                  uint32_t *__restrict__ out, StencilParams p,
                                                  unsigned long long *__restrict__ slots) {
@@ -692,6 +720,10 @@ __global__ __launch_bounds__(256) void gol_step1(const uint32_t *__restrict__ in
         out + (int64_t)ya * p.pitch, 0, (yb - ya) * rowbytes, kBufferRsrcWord3);
     const bool owned = colraw < p.wd;
     const int off = owned ? col * 4 : kOutOfRange;
+    __amdgpu_buffer_rsrc_t drsrc = orsrc;  // LD: the generation's flips beside the output
+    if constexpr (LD)
+        drsrc = __builtin_amdgcn_make_buffer_rsrc(p.diff + (int64_t)ya * p.pitch, 0,
+                                                  (yb - ya) * rowbytes, kBufferRsrcWord3);
 
     RowStream rows(p, ya - 1);
     uint4 buf[P];
@@ -743,6 +775,12 @@ __global__ __launch_bounds__(256) void gol_step1(const uint32_t *__restrict__ in
             const v4i v = {(int)nx.w[0], (int)nx.w[1], (int)nx.w[2], (int)nx.w[3]};
             __builtin_amdgcn_raw_buffer_store_b128(v, orsrc, off + (live ? r * rowbytes : kOutOfRange), 0,
                                                    (NT & 2) ? 2 /* nt */ : 0);
+            if constexpr (LD) {
+                const v4i dv = {(int)(nx.w[0] ^ mc.w[0]), (int)(nx.w[1] ^ mc.w[1]),
+                                (int)(nx.w[2] ^ mc.w[2]), (int)(nx.w[3] ^ mc.w[3])};
+                __builtin_amdgcn_raw_buffer_store_b128(dv, drsrc, off + (live ? r * rowbytes : kOutOfRange),
+                                                       0, (NT & 2) ? 2 : 0);
+            }
             if (COUNT && live && owned)
                 acc += __builtin_popcount(nx.w[0]) + __builtin_popcount(nx.w[1]) +
                        __builtin_popcount(nx.w[2]) + __builtin_popcount(nx.w[3]);
@@ -768,7 +806,7 @@ __global__ __launch_bounds__(256) void gol_step1(const uint32_t *__restrict__ in
 // K/S levels and the board runs S times as many waves, with no extra (halo) work.
 // Wave R's level j outputs row ya - K + st - (j+1) - R at step st (one step of delay per hand-off),
 // valid from step 2j + 2 + R; the final row (j = K-1, R = S-1) lags by 2K + S - 1 steps.
-template <int K, bool COUNT, int S, int R>
+template <int K, bool COUNT, int S, int R, bool LD = false>
 __device__ __forceinline__ void split_role(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
                                            const StencilParams &p,
                                            unsigned long long *__restrict__ slots, int64_t group,
@@ -790,6 +828,11 @@ __device__ __forceinline__ void split_role(const uint32_t *__restrict__ in, uint
     const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
         out + (int64_t)ya * p.pitch, 0, (yb - ya) * rowbytes, kBufferRsrcWord3);
     const LaneStore ls = lane_store<HH>(lane, colraw, col, p.wd);
+    __amdgpu_buffer_rsrc_t drsrc = orsrc;  // LD: the last generation's flips beside the output
+    if constexpr (LD)
+        drsrc = __builtin_amdgcn_make_buffer_rsrc(p.diff + (int64_t)ya * p.pitch, 0,
+                                                  (yb - ya) * rowbytes, kBufferRsrcWord3);
+    uint32_t midc = 0;  // LD: the step's last-level output XOR its mid row's centre cells
     const bool count_lane = lane >= 1 && colraw < p.wd;  // DR count window (see gol_stencil)
     RowStream rows(p, ya - K);
 
@@ -838,6 +881,8 @@ __device__ __forceinline__ void split_role(const uint32_t *__restrict__ in, uint
                 level_update<1, DR>(X[jl], Y[jl], nc, nx);
             else
                 level_update<1, DR>(Y[jl], X[jl], nc, nx);
+            if (LD && R == S - 1 && jl == NL - 1)  // last level: the generation before, same frame
+                midc = nx.w[0] ^ (PAR == 0 ? Y[jl] : X[jl]).c.w[0];
             if (COUNT) {
                 const int rr = st - K - (j + 1) - R;
                 const uint32_t m = DR ? ~0u : ls.own_mask;
@@ -849,9 +894,16 @@ __device__ __forceinline__ void split_role(const uint32_t *__restrict__ in, uint
             xring[R][st & 1][lane] = nc.w[0];
         } else {
             const int rr = st - LAG;
-            if constexpr (DR)  // back to the board frame: K bits west
-                nc.w[0] = __builtin_amdgcn_alignbit(lane_from_east(nc.w[0]), nc.w[0], K);
+            if constexpr (DR) {  // back to the board frame: K bits west
+                nc.w[0] = realign_drift<K>(nc.w[0]);
+                if constexpr (LD) midc = realign_drift<K>(midc);
+            }
             store_row<1, HH>(orsrc, ls, nc, (rr >= 0 && rr < nrows) ? rr * rowbytes : kOutOfRange);
+            if constexpr (LD) {
+                Words<1> dv;
+                dv.w[0] = midc;
+                store_row<1, HH>(drsrc, ls, dv, (rr >= 0 && rr < nrows) ? rr * rowbytes : kOutOfRange);
+            }
         }
         // hand-off visible to the next wave, and this step's reads done before slots are reused
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -884,7 +936,7 @@ __device__ __forceinline__ void split_role(const uint32_t *__restrict__ in, uint
     }
 }
 
-template <int K, bool COUNT, int S>
+template <int K, bool COUNT, int S, bool LD = false>
 __global__ __launch_bounds__(64 * S) void gol_stencil_split(const uint32_t *__restrict__ in,
                                                             uint32_t *__restrict__ out,
                                                             StencilParams p,
@@ -898,7 +950,7 @@ __global__ __launch_bounds__(64 * S) void gol_stencil_split(const uint32_t *__re
     const int r = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     static_for(std::make_integer_sequence<int, S>{}, [&](auto rc) {
         constexpr int RR = decltype(rc)::value;
-        if (r == RR) split_role<K, COUNT, S, RR>(in, out, p, slots, group, lane, xring, ring);
+        if (r == RR) split_role<K, COUNT, S, RR, LD>(in, out, p, slots, group, lane, xring, ring);
     });
 }
 template <int K, int D>
@@ -917,7 +969,11 @@ template <int P, int NT>
 hipError_t launch_step1_cfg(const uint32_t *in, uint32_t *out, const StencilParams &p,
                             unsigned long long *slots, hipStream_t s) {
     const unsigned blocks = (unsigned)std::max<int64_t>(1, (p.nbands * (int64_t)p.nchunks + 3) / 4);
-    if (slots)
+    if (p.diff && slots)
+        hipLaunchKernelGGL((gol_step1<true, P, NT, true>), dim3(blocks), dim3(256), 0, s, in, out, p, slots);
+    else if (p.diff)
+        hipLaunchKernelGGL((gol_step1<false, P, NT, true>), dim3(blocks), dim3(256), 0, s, in, out, p, slots);
+    else if (slots)
         hipLaunchKernelGGL((gol_step1<true, P, NT>), dim3(blocks), dim3(256), 0, s, in, out, p, slots);
     else
         hipLaunchKernelGGL((gol_step1<false, P, NT>), dim3(blocks), dim3(256), 0, s, in, out, p, slots);
@@ -947,13 +1003,26 @@ inline const void *step1_fn() {
 }
 
 template <int K, bool SKEW, int D, int PF = 0, bool DR = false, int ZIP = 1, bool HH = kHalfHalo<K, D>,
-          bool FILLU = true>
+          bool FILLU = true, bool ALLOW_LD = false>
 hipError_t launch_stencil_k(const uint32_t *in, uint32_t *out, const StencilParams &p,
                             unsigned long long *slots, hipStream_t s) {
     const int64_t waves = p.nbands * (int64_t)p.nchunks;
     // at least one block: an empty launch (nbands = 0, every wave returns at once) is how
     // warm_stencil_k loads this depth's code object before anything is timed
     const unsigned blocks = (unsigned)std::max<int64_t>(1, (waves + 3) / 4);
+    if (p.diff) {  // last-generation flips beside the output (production variants only)
+        if constexpr (ALLOW_LD) {
+            if (slots)
+                hipLaunchKernelGGL((gol_stencil<K, true, SKEW, D, PF, HH, DR, ZIP, FILLU, true>),
+                                   dim3(blocks), dim3(256), lds_pad_bytes(), s, in, out, p, slots);
+            else
+                hipLaunchKernelGGL((gol_stencil<K, false, SKEW, D, PF, HH, DR, ZIP, FILLU, true>),
+                                   dim3(blocks), dim3(256), lds_pad_bytes(), s, in, out, p, slots);
+            return hipGetLastError();
+        } else {
+            return hipErrorNotSupported;
+        }
+    }
     if (slots)
         hipLaunchKernelGGL((gol_stencil<K, true, SKEW, D, PF, HH, DR, ZIP, FILLU>), dim3(blocks), dim3(256),
                            lds_pad_bytes(), s, in, out, p, slots);
@@ -978,15 +1047,15 @@ hipError_t launch_variant(int variant, const uint32_t *in, uint32_t *out, const 
         case kVariantChainLdsD2: return launch_stencil_k<K, false, 2, 1>(in, out, p, slots, s);
         case kVariantDriftLds:
             if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
-            else if constexpr (K > 16) return launch_stencil_k<K, false, 1, 1>(in, out, p, slots, s);
-            else return launch_stencil_k<K, false, 1, 1, true>(in, out, p, slots, s);
+            else if constexpr (K > 16) return launch_stencil_k<K, false, 1, 1, false, 1, kHalfHalo<K, 1>, true, true>(in, out, p, slots, s);
+            else return launch_stencil_k<K, false, 1, 1, true, 1, true, true, true>(in, out, p, slots, s);
         case kVariantDrift62:
             if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
-            else return launch_stencil_k<K, false, 1, 1, true, 1, false>(in, out, p, slots, s);
+            else return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true>(in, out, p, slots, s);
         case kVariantProd:  // per depth: the fastest measured (golhip_internal.hpp)
             if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
-            else if constexpr (prod_half_halo(K)) return launch_stencil_k<K, false, 1, 1, true, 1, true>(in, out, p, slots, s);
-            else return launch_stencil_k<K, false, 1, 1, true, 1, false>(in, out, p, slots, s);
+            else if constexpr (prod_half_halo(K)) return launch_stencil_k<K, false, 1, 1, true, 1, true, true, true>(in, out, p, slots, s);
+            else return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true>(in, out, p, slots, s);
         case kVariantDriftNoFill:
             if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
             else return launch_stencil_k<K, false, 1, 1, (K <= 16), 1, kHalfHalo<K, 1>, false>(in, out, p, slots, s);
@@ -1034,7 +1103,13 @@ hipError_t launch_split_ks(const uint32_t *in, uint32_t *out, const StencilParam
                            unsigned long long *slots, hipStream_t s) {
     const unsigned blocks = (unsigned)(p.nbands * (int64_t)p.nchunks);
     if (blocks == 0) return hipSuccess;
-    if (slots)
+    if (p.diff && slots)
+        hipLaunchKernelGGL((gol_stencil_split<K, true, S, true>), dim3(blocks), dim3(64 * S), 0, s,
+                           in, out, p, slots);
+    else if (p.diff)
+        hipLaunchKernelGGL((gol_stencil_split<K, false, S, true>), dim3(blocks), dim3(64 * S), 0, s,
+                           in, out, p, slots);
+    else if (slots)
         hipLaunchKernelGGL((gol_stencil_split<K, true, S>), dim3(blocks), dim3(64 * S), 0, s, in,
                            out, p, slots);
     else

@@ -39,7 +39,9 @@ EXPORTS = [
     "golhip_store_bytes", "golhip_store_words", "golhip_load_words", "golhip_step",
     "golhip_alive_count", "golhip_alive_cells", "golhip_flips", "golhip_turn",
     "golhip_set_turn", "golhip_set_k", "golhip_set_band_rows", "golhip_sync", "golhip_timing",
-    "golhip_kernel_time", "golhip_launch_plan", "golhip_set_fixed_k",
+    "golhip_kernel_time", "golhip_launch_plan", "golhip_set_fixed_k", "golhip_track_flips",
+    "golhip_step_flips", "golhip_flips_ring_capacity", "golhip_flips_fetch",
+    "golhip_checkpoint_save", "golhip_checkpoint_load", "golhip_checkpoint_info",
 ]
 
 
@@ -105,6 +107,15 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
         "golhip_set_k": ([H, i32], i32),
         "golhip_set_band_rows": ([H, i32], i32),
         "golhip_set_fixed_k": ([H, i32], i32),
+        "golhip_track_flips": ([H, i32], i32),
+        "golhip_checkpoint_save": ([H, ctypes.c_char_p], i32),
+        "golhip_checkpoint_load": ([H, ctypes.c_char_p], i32),
+        "golhip_checkpoint_info": ([ctypes.c_char_p, i64p, i64p, i64p], i32),
+        "golhip_step_flips": ([H, i64, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
+                               ctypes.c_void_p, ctypes.c_void_p], i32),
+        "golhip_flips_ring_capacity": ([H, i64p], i32),
+        "golhip_flips_fetch": ([H, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
+                                ctypes.c_void_p], i32),
         "golhip_sync": ([H], i32),
         "golhip_timing": ([H, i32], i32),
         "golhip_kernel_time": ([H, ctypes.POINTER(ctypes.c_double), i64p, i64p], i32),
@@ -193,6 +204,16 @@ def launch_plan(width: int, height: int, k: int, turns: int, strips: int = 1) ->
     if rc != OK:
         raise GolHipError(rc, "launch_plan failed")
     return [int(x) for x in out[: n.value]]
+
+
+def checkpoint_info(path) -> tuple[int, int, int]:
+    """(width, height, turn) of a checkpoint file (pure host, no device)."""
+    w, h, t = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    rc = load_library().golhip_checkpoint_info(str(path).encode(), ctypes.byref(w), ctypes.byref(h),
+                                               ctypes.byref(t))
+    if rc != OK:
+        raise GolHipError(rc, f"{path}: not a golhip checkpoint")
+    return w.value, h.value, t.value
 
 
 def nccl_unique_id() -> bytes:
@@ -307,6 +328,45 @@ class Engine:
     def flips(self) -> np.ndarray:
         """(n, 2) int32 array of (x, y) that changed in the last generation."""
         return self._cells(self._L.golhip_flips)
+
+    def checkpoint_save(self, path):
+        self._check(self._L.golhip_checkpoint_save(self._h, str(path).encode()))
+
+    def checkpoint_load(self, path):
+        self._check(self._L.golhip_checkpoint_load(self._h, str(path).encode()))
+
+    def track_flips(self, enable: bool = True):
+        """Keep the last generation's flips on every step (golhip_flips valid after a K-deep step)."""
+        self._check(self._L.golhip_track_flips(self._h, int(enable)))
+
+    def flips_ring_capacity(self) -> int:
+        v = ctypes.c_int64()
+        self._check(self._L.golhip_flips_ring_capacity(self._h, ctypes.byref(v)))
+        return v.value
+
+    def step_flips(self, turns: int, counts: bool = False):
+        """Advance `turns` keeping every turn's flips: returns (list of per-turn (n_t, 2) views of
+        a host buffer reused by the next call, alive counts per turn or None)."""
+        n = ctypes.c_size_t(0)
+        per = np.zeros(max(turns, 1), dtype=np.uint64)
+        alive = np.zeros(max(turns, 1), dtype=np.uint64) if counts else None
+        # one host list reused across calls (a fresh multi-100-MB array per call would spend its
+        # time in page faults): filled directly when it fits, else grown and fetched
+        buf = getattr(self, "_flip_buf", None)
+        if buf is None:
+            buf = self._flip_buf = np.zeros((1 << 16, 2), dtype=np.int32)
+        rc = self._L.golhip_step_flips(self._h, turns, buf.ctypes.data, len(buf), ctypes.byref(n),
+                                       per.ctypes.data, alive.ctypes.data if counts else None)
+        if rc == ERR_CAP:
+            buf = self._flip_buf = np.zeros((max(n.value, 2 * len(buf)), 2), dtype=np.int32)
+            self._check(self._L.golhip_flips_fetch(self._h, buf.ctypes.data, len(buf),
+                                                   ctypes.byref(n), per.ctypes.data))
+        else:
+            self._check(rc)
+        xy = buf
+        bounds = np.concatenate([[0], np.cumsum(per[:turns])]).astype(np.int64)
+        out = [xy[bounds[t]:bounds[t + 1]] for t in range(turns)]
+        return out, (alive[:turns] if counts else None)
 
     @property
     def turn(self) -> int:

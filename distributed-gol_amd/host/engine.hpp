@@ -2,6 +2,7 @@
 // Host code only: no HIP headers, exactly what a cgo/JNI/ctypes caller would see.
 #pragma once
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -53,6 +54,30 @@ public:
     }
     std::vector<int32_t> alive_cells() { return cells(golhip_alive_cells); }
     std::vector<int32_t> flips() { return cells(golhip_flips); }
+    // Per-turn flips of `turns` turns (<= flips_ring_capacity()): xy = every turn's cells, turn
+    // by turn; per_turn[t] = cells of turn t; alive[t] = alive after turn t.
+    void step_flips(int64_t turns, std::vector<int32_t> &xy, std::vector<uint64_t> &per_turn,
+                    std::vector<uint64_t> &alive) {
+        per_turn.resize((size_t)turns);
+        alive.resize((size_t)turns);
+        size_t n = 0;
+        if (xy.size() < 2) xy.resize(2 << 16);
+        int rc = golhip_step_flips(h_, turns, xy.data(), xy.size() / 2, &n, per_turn.data(),
+                                   alive.data());
+        if (rc == GOLHIP_ERR_CAP) {  // the turns ran; fetch into a larger list
+            xy.resize(2 * std::max(n, xy.size()));
+            rc = golhip_flips_fetch(h_, xy.data(), xy.size() / 2, &n, per_turn.data());
+        }
+        check(rc);
+    }
+    int64_t flips_ring_capacity() {
+        int64_t c = 1;
+        check(golhip_flips_ring_capacity(h_, &c));
+        return c;
+    }
+    void track_flips(bool on) { check(golhip_track_flips(h_, on ? 1 : 0)); }
+    void checkpoint_save(const std::string &path) { check(golhip_checkpoint_save(h_, path.c_str())); }
+    void checkpoint_load(const std::string &path) { check(golhip_checkpoint_load(h_, path.c_str())); }
     int64_t turn() {
         int64_t t = 0;
         check(golhip_turn(h_, &t));

@@ -2,12 +2,13 @@
 //
 // Reference flow (gol/distributor.go:194-263) and what replaces each part here:
 //   read images/WxH.pgm, CellFlipped for initially alive cells  :204-216  -> same
-//   rpc.Dial(broker) + makeCall/CheckStates resume              :218,69-91 -> Engine (+ saved
-//                                                                             state of 'q')
-//   Call(): per turn Broker.Publish, O(N^2) diff -> CellFlipped :45-67     -> golhip_step(1) +
-//                                                                             golhip_flips, or
-//                                                                             chunked
-//                                                                             golhip_step(n)
+//   rpc.Dial(broker) + makeCall/CheckStates resume              :218,69-91 -> Engine + the
+//                                                                             checkpoint file
+//                                                                             'q' wrote
+//   Call(): per turn Broker.Publish, O(N^2) diff -> CellFlipped :45-67     -> chunked
+//                                                                             golhip_step_flips
+//                                                                             (per-turn flips)
+//                                                                             or golhip_step(n)
 //   countAliveCells: O(N^2) scan per turn, 2 s ticker           :168-191   -> per-turn counts
 //                                                                             from the stencil
 //   manageKeyPresses s/q/p/k                                    :105-151   -> serviced between
@@ -19,6 +20,7 @@
 // always sends 0); the 's' snapshot is named with the completed turn; a tick before the first
 // completed turn reports the initial count; 'q' and 'k' end Run() (closing `events`) instead of
 // leaving the turn loop running.
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -52,41 +54,41 @@ std::string Event::String() const {
     }
 }
 
-Event Event::alive_cells_count(int t, int64_t n) {
+Event Event::alive_cells_count(int64_t t, int64_t n) {
     Event e;
     e.kind = EventKind::AliveCellsCount;
     e.CompletedTurns = t;
     e.CellsCount = n;
     return e;
 }
-Event Event::image_output_complete(int t, std::string f) {
+Event Event::image_output_complete(int64_t t, std::string f) {
     Event e;
     e.kind = EventKind::ImageOutputComplete;
     e.CompletedTurns = t;
     e.Filename = std::move(f);
     return e;
 }
-Event Event::state_change(int t, State s) {
+Event Event::state_change(int64_t t, State s) {
     Event e;
     e.kind = EventKind::StateChange;
     e.CompletedTurns = t;
     e.NewState = s;
     return e;
 }
-Event Event::cell_flipped(int t, Cell c) {
+Event Event::cell_flipped(int64_t t, Cell c) {
     Event e;
     e.kind = EventKind::CellFlipped;
     e.CompletedTurns = t;
     e.cell = c;
     return e;
 }
-Event Event::turn_complete(int t) {
+Event Event::turn_complete(int64_t t) {
     Event e;
     e.kind = EventKind::TurnComplete;
     e.CompletedTurns = t;
     return e;
 }
-Event Event::final_turn_complete(int t, std::vector<Cell> alive) {
+Event Event::final_turn_complete(int64_t t, std::vector<Cell> alive) {
     Event e;
     e.kind = EventKind::FinalTurnComplete;
     e.CompletedTurns = t;
@@ -96,16 +98,6 @@ Event Event::final_turn_complete(int t, std::vector<Cell> alive) {
 
 namespace {
 
-// The broker's pause state (broker/broker.go:33-35 worldSave/turn/size), kept device-resident:
-// 'q' parks the engine here; the next Run() of the same size resumes from it (CheckStates).
-struct Saved {
-    std::unique_ptr<Engine> engine;
-    int width = 0, height = 0;
-    int turn = 0;
-};
-std::mutex g_saved_mu;
-Saved g_saved;
-
 std::vector<Cell> to_cells(const std::vector<int32_t> &xy) {
     std::vector<Cell> out(xy.size() / 2);
     for (size_t i = 0; i < out.size(); ++i) out[i] = {xy[2 * i], xy[2 * i + 1]};
@@ -114,10 +106,12 @@ std::vector<Cell> to_cells(const std::vector<int32_t> &xy) {
 
 struct Ticker {  // gol/distributor.go:168-191 with the 2 s time.Ticker of :228
     std::mutex mu;
-    int turn = 0;
+    int64_t turn = 0;
     int64_t count = 0;
     std::atomic<bool> stop{false};
     std::thread th;
+
+    ~Ticker() { halt(); }  // an exception unwinding Run must not destroy a joinable thread
 
     void start(Channel<Event> *events, int period_ms) {
         th = std::thread([this, events, period_ms] {
@@ -126,8 +120,7 @@ struct Ticker {  // gol/distributor.go:168-191 with the 2 s time.Ticker of :228
                 std::this_thread::sleep_for(std::chrono::milliseconds(5));
                 if (std::chrono::steady_clock::now() < next) continue;
                 next += std::chrono::milliseconds(period_ms);
-                int t;
-                int64_t c;
+                int64_t t, c;
                 {
                     std::lock_guard<std::mutex> lk(mu);
                     t = turn;
@@ -141,7 +134,7 @@ struct Ticker {  // gol/distributor.go:168-191 with the 2 s time.Ticker of :228
             }
         });
     }
-    void update(int t, int64_t c) {
+    void update(int64_t t, int64_t c) {
         std::lock_guard<std::mutex> lk(mu);
         turn = t;
         count = c;
@@ -161,37 +154,67 @@ void snapshot(Engine &eng, const Params &p, const RunOptions &o, const std::stri
     write_pgm(o.out_dir + "/" + name + ".pgm", img);
 }
 
-}  // namespace
-
-void reset_saved_state() {
-    std::lock_guard<std::mutex> lk(g_saved_mu);
-    g_saved = Saved{};
+bool file_exists(const std::string &path) {
+    if (FILE *f = std::fopen(path.c_str(), "rb")) {
+        std::fclose(f);
+        return true;
+    }
+    return false;
 }
 
+void run_impl(const Params &p, Channel<Event> *events, Channel<char> *keyPresses,
+              const RunOptions &o);
+
+}  // namespace
+
+std::string checkpoint_file(const RunOptions &o) {
+    return o.checkpoint_path.empty() ? o.out_dir + "/broker_state.ckpt" : o.checkpoint_path;
+}
+
+void reset_saved_state(const RunOptions &o) { std::remove(checkpoint_file(o).c_str()); }
+
 void Run(Params p, Channel<Event> *events, Channel<char> *keyPresses, const RunOptions &o) {
+    // A failure (EngineError, I/O) ends the run the way the reference's controller ends: the
+    // events channel is closed so consumers see the end, then the error propagates.
+    try {
+        run_impl(p, events, keyPresses, o);
+    } catch (...) {
+        events->close();
+        throw;
+    }
+}
+
+namespace {
+
+void run_impl(const Params &p, Channel<Event> *events, Channel<char> *keyPresses,
+              const RunOptions &o) {
     const std::string name = board_name(p);
     Image img = read_pgm(o.image_dir + "/" + name + ".pgm");
     if (img.width != p.ImageWidth) throw std::runtime_error("Incorrect width");
     if (img.height != p.ImageHeight) throw std::runtime_error("Incorrect height");
 
-    int turn = 0;
+    int64_t turn = 0;
     const std::vector<Cell> initial = alive_cells_of(img);
     if (o.flip_events)  // gol/distributor.go:212-214
         for (const Cell &c : initial) events->send(Event::cell_flipped(0, c));
 
-    // makeCall: resume a board parked by 'q' when the size matches (gol/distributor.go:69-91,
-    // broker/broker.go:124-141); CheckStates clears the saved state either way.
-    std::unique_ptr<Engine> eng;
-    if (p.Turns > 0) {
-        std::lock_guard<std::mutex> lk(g_saved_mu);
-        if (g_saved.engine && g_saved.width == p.ImageWidth && g_saved.height == p.ImageHeight) {
-            eng = std::move(g_saved.engine);
-            turn = g_saved.turn;
+    // makeCall (gol/distributor.go:69-91): with Turns > 0, CheckStates consumes the broker's
+    // paused state -- here the checkpoint file -- and resumes from it when the size matches
+    // (broker/broker.go:124-141 clears `paused` either way).
+    auto eng = std::make_unique<Engine>(p.ImageWidth, p.ImageHeight, o.ngpus, o.k);
+    bool resumed = false;
+    const std::string ckpt = checkpoint_file(o);
+    if (p.Turns > 0 && file_exists(ckpt)) {
+        int64_t cw = 0, ch = 0, ct = 0;
+        if (golhip_checkpoint_info(ckpt.c_str(), &cw, &ch, &ct) == GOLHIP_OK && cw == p.ImageWidth &&
+            ch == p.ImageHeight) {
+            eng->checkpoint_load(ckpt);
+            turn = ct;
+            resumed = true;
         }
-        g_saved = Saved{};
+        std::remove(ckpt.c_str());
     }
-    if (!eng) {
-        eng = std::make_unique<Engine>(p.ImageWidth, p.ImageHeight, o.ngpus, o.k);
+    if (!resumed) {
         for (auto &px : img.pixels) px = px ? 255 : 0;
         eng->load(img.pixels);
     }
@@ -212,14 +235,10 @@ void Run(Params p, Channel<Event> *events, Channel<char> *keyPresses, const RunO
                 break;
             }
             case 'q': {
+                // Pause{P: true, Turn, Dimension} parks the state in the broker (:139-147): the
+                // checkpoint file outlives this process; a later Run resumes from it
+                eng->checkpoint_save(ckpt);
                 events->send(Event::state_change(turn, State::Quitting));
-                {
-                    std::lock_guard<std::mutex> lk(g_saved_mu);
-                    g_saved.engine = std::move(eng);
-                    g_saved.width = p.ImageWidth;
-                    g_saved.height = p.ImageHeight;
-                    g_saved.turn = turn;
-                }
                 quit = true;
                 break;
             }
@@ -229,7 +248,7 @@ void Run(Params p, Channel<Event> *events, Channel<char> *keyPresses, const RunO
                 events->send(Event::image_output_complete(turn, f));
                 events->send(Event::state_change(turn, State::Quitting));
                 eng.reset();  // Broker.Quit -> GolOP.Quit: the workers go away
-                reset_saved_state();
+                reset_saved_state(o);
                 quit = true;
                 break;
             }
@@ -241,9 +260,12 @@ void Run(Params p, Channel<Event> *events, Channel<char> *keyPresses, const RunO
         }
     };
 
-    const int W = p.ImageWidth, H = p.ImageHeight;
-    (void)W;
-    (void)H;
+    // Per-turn CellFlipped: chunks of turns through golhip_step_flips (each turn's flips kept in
+    // a device ring, one extraction per chunk); chunk sizes grow while a chunk takes less than
+    // chunk_seconds, so keys still wait at most about that long.
+    const int64_t ring_cap = o.flip_events ? eng->flips_ring_capacity() : 1;
+    std::vector<int32_t> fxy;
+    std::vector<uint64_t> fper, falive;
     int64_t chunk = 1;
     bool paused = false;
     while (!quit && turn < p.Turns) {
@@ -256,29 +278,32 @@ void Run(Params p, Channel<Event> *events, Channel<char> *keyPresses, const RunO
             }
         }
         if (quit) break;
+        const auto t0 = std::chrono::steady_clock::now();
         if (o.flip_events) {
-            // one turn: step, diff -> CellFlipped{turn}, TurnComplete{turn+1}
-            const std::vector<uint64_t> c = eng->step(1, true);
-            for (const Cell &cell : to_cells(eng->flips()))
-                events->send(Event::cell_flipped(turn, cell));
-            ++turn;
-            ticker.update(turn, (int64_t)c[0]);
-            events->send(Event::turn_complete(turn));
+            // per turn: CellFlipped{turn} for each flipped cell, then TurnComplete{turn+1}
+            const int64_t n = std::min<int64_t>({chunk, p.Turns - turn, ring_cap});
+            eng->step_flips(n, fxy, fper, falive);
+            size_t at = 0;
+            for (int64_t i = 0; i < n; ++i) {
+                for (uint64_t c = 0; c < fper[(size_t)i]; ++c, ++at)
+                    events->send(Event::cell_flipped(turn, Cell{fxy[2 * at], fxy[2 * at + 1]}));
+                ++turn;
+                ticker.update(turn, (int64_t)falive[(size_t)i]);
+                events->send(Event::turn_complete(turn));
+            }
         } else {
             const int64_t n = std::min<int64_t>(chunk, p.Turns - turn);
-            const auto t0 = std::chrono::steady_clock::now();
             const std::vector<uint64_t> c = eng->step(n, true);
             for (int64_t i = 0; i < n; ++i) {
-                ticker.update(turn + (int)i + 1, (int64_t)c[(size_t)i]);
-                events->send(Event::turn_complete(turn + (int)i + 1));
+                ticker.update(turn + i + 1, (int64_t)c[(size_t)i]);
+                events->send(Event::turn_complete(turn + i + 1));
             }
-            turn += (int)n;
-            // chunk sized on device time + event delivery, so keys wait at most ~chunk_seconds
-            const double dt =
-                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-            if (dt < o.chunk_seconds && chunk < (1 << 20)) chunk *= 2;
-            if (dt > 4 * o.chunk_seconds && chunk > 1) chunk /= 2;
+            turn += n;
         }
+        // chunk sized on device time + event delivery, so keys wait at most ~chunk_seconds
+        const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (dt < o.chunk_seconds && chunk < (1 << 20)) chunk *= 2;
+        if (dt > 4 * o.chunk_seconds && chunk > 1) chunk /= 2;
     }
 
     if (quit) {  // 'q' / 'k': FinalTurnComplete with no cells (gol/distributor.go:128,147)
@@ -295,6 +320,8 @@ void Run(Params p, Channel<Event> *events, Channel<char> *keyPresses, const RunO
     events->send(Event::state_change(turn, State::Quitting));   // :259
     events->close();                                             // :262
 }
+
+}  // namespace
 
 int Publish(const Request &req, Response *res, int ngpus) {
     static std::mutex mu;

@@ -30,9 +30,9 @@ struct Cell {
     bool operator<(const Cell &o) const { return Y != o.Y ? Y < o.Y : X < o.X; }
 };
 
-// gol/gol.go:6-11
+// gol/gol.go:6-11 (Go's int is 64-bit: Turns defaults to 1e10 in main.go:38-42)
 struct Params {
-    int Turns = 0;
+    int64_t Turns = 0;
     int Threads = 1;  // kept for contract parity; the GPU grid replaces goroutine strips
     int ImageWidth = 0;
     int ImageHeight = 0;
@@ -54,7 +54,7 @@ enum class EventKind {
 
 struct Event {
     EventKind kind = EventKind::TurnComplete;
-    int CompletedTurns = 0;
+    int64_t CompletedTurns = 0;  // Go int
     int64_t CellsCount = 0;
     std::string Filename;
     State NewState = State::Executing;
@@ -63,14 +63,14 @@ struct Event {
 
     // gol/event.go:71-131: the GUI prints events whose String() is non-empty (sdl/loop.go:44-47)
     std::string String() const;
-    int GetCompletedTurns() const { return CompletedTurns; }
+    int64_t GetCompletedTurns() const { return CompletedTurns; }
 
-    static Event alive_cells_count(int turns, int64_t n);
-    static Event image_output_complete(int turns, std::string f);
-    static Event state_change(int turns, State s);
-    static Event cell_flipped(int turns, Cell c);
-    static Event turn_complete(int turns);
-    static Event final_turn_complete(int turns, std::vector<Cell> alive);
+    static Event alive_cells_count(int64_t turns, int64_t n);
+    static Event image_output_complete(int64_t turns, std::string f);
+    static Event state_change(int64_t turns, State s);
+    static Event cell_flipped(int64_t turns, Cell c);
+    static Event turn_complete(int64_t turns);
+    static Event final_turn_complete(int64_t turns, std::vector<Cell> alive);
 };
 
 // stubs/stubs.go:15-29 (the broker wire types; World rows of 0/255 bytes)
@@ -94,6 +94,10 @@ struct RunOptions {
     bool flip_events = true;           // per-turn CellFlipped (gol/distributor.go:53-59)
     int ticker_ms = 2000;              // AliveCellsCount period (gol/distributor.go:228)
     double chunk_seconds = 0.02;       // target device time per step chunk (key/ticker latency)
+    // The broker's paused state (worldSave, turn, size; broker/broker.go:124-155) as a file: 'q'
+    // writes it, the next Run with Turns > 0 consumes it (CheckStates) and resumes when the size
+    // matches.  Empty: <out_dir>/broker_state.ckpt.
+    std::string checkpoint_path;
 };
 
 // gol/gol.go:14 -- runs the whole simulation, sends events, closes `events` at the end.
@@ -106,7 +110,8 @@ void Run(Params p, Channel<Event> *events, Channel<char> *keyPresses,
 int Publish(const Request &req, Response *res, int ngpus = 1);
 
 // Forget a board saved by 'q' (broker/broker.go:124-141 CheckStates clears `paused`).
-void reset_saved_state();
+void reset_saved_state(const RunOptions &opts = RunOptions());
+std::string checkpoint_file(const RunOptions &opts);
 
 // gol/io.go helpers (P5, maxval 255).
 struct Image {

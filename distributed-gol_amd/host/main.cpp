@@ -1,6 +1,7 @@
 // main.cpp -- headless CLI mirroring the reference's main.go:13-68 flags on the C++ host.
 //   -t threads  -w width  -h height  -turns N  -noVis (always headless: SDL is out of scope)
-//   extra: -gpus G (row strips), -k K (generations per launch), -images DIR, -out DIR
+//   extra: -gpus G (row strips), -k K (max generations per launch), -images DIR, -out DIR,
+//          -checkpoint PATH (the 'q' state file; default OUT/broker_state.ckpt), -flips
 // Keys p/s/q/k are read from stdin (one character per line), like the SDL key loop
 // (sdl/loop.go:17-27) would deliver them.
 #include <cstdio>
@@ -13,7 +14,7 @@
 #include "gol.hpp"
 
 int main(int argc, char **argv) {
-    gol::Params p{1000000000, 8, 512, 512};  // main.go defaults: 8 threads, 512x512, 1e10 turns
+    gol::Params p{10000000000LL, 8, 512, 512};  // main.go:38-42 defaults: 8 threads, 512x512, 1e10 turns
     gol::RunOptions o;
     o.flip_events = false;
     for (int i = 1; i < argc; ++i) {
@@ -22,11 +23,12 @@ int main(int argc, char **argv) {
         if (a == "-t") p.Threads = std::atoi(next());
         else if (a == "-w") p.ImageWidth = std::atoi(next());
         else if (a == "-h") p.ImageHeight = std::atoi(next());
-        else if (a == "-turns") p.Turns = std::atoi(next());
+        else if (a == "-turns") p.Turns = std::strtoll(next(), nullptr, 10);  // Go int: 64-bit
         else if (a == "-gpus") o.ngpus = std::atoi(next());
         else if (a == "-k") o.k = std::atoi(next());
         else if (a == "-images") o.image_dir = next();
         else if (a == "-out") o.out_dir = next();
+        else if (a == "-checkpoint") o.checkpoint_path = next();
         else if (a == "-flips") o.flip_events = true;
         else if (a == "-noVis") {}
     }
@@ -44,9 +46,11 @@ int main(int argc, char **argv) {
     std::thread run([&] { gol::Run(p, &events, &keys, o); });
     while (auto e = events.recv()) {
         const std::string s = e->String();
-        if (!s.empty()) std::printf("Completed Turns %-8d%s\n", e->GetCompletedTurns(), s.c_str());
+        if (!s.empty())
+            std::printf("Completed Turns %-8lld%s\n", (long long)e->GetCompletedTurns(), s.c_str());
         if (e->kind == gol::EventKind::FinalTurnComplete)
-            std::printf("Final turn %d: %zu alive cells\n", e->CompletedTurns, e->Alive->size());
+            std::printf("Final turn %lld: %zu alive cells\n", (long long)e->CompletedTurns,
+                        e->Alive->size());
     }
     run.join();
     std::fflush(stdout);

@@ -119,6 +119,19 @@ int golhip_store_bytes(golhip_t h, uint8_t *out, size_t row_stride);
 int golhip_store_words(golhip_t h, uint64_t *out);
 int golhip_load_words(golhip_t h, const uint64_t *in);
 
+/* ---- checkpoint: the broker's paused state (broker/broker.go:124-155) ---------------------
+ * The reference keeps worldSave/turn/size in the broker process between controller runs ('q'
+ * sends Pause{P: true, Turn, Dimension}; the next controller's CheckStates resumes when the size
+ * matches, gol/distributor.go:69-91).  Here that state is a file: the handle's rows as packed
+ * bits (64-byte header: "GOLCKPT1", version 1, width, height, y0, rows, turn, row bytes; then
+ * rows x ceil(width/8) bytes, LSB-first) and the completed turn, written atomically (tmp +
+ * rename).  A rank-mode handle writes/loads its own strip (one file per rank). */
+int golhip_checkpoint_save(golhip_t h, const char *path);
+/* Restores the board and turn; GOLHIP_ERR_STATE if the file holds another board or strip. */
+int golhip_checkpoint_load(golhip_t h, const char *path);
+/* Pure host helper: the board size and turn a checkpoint holds (CheckStates' SameSize test). */
+int golhip_checkpoint_info(const char *path, int64_t *width, int64_t *height, int64_t *turn);
+
 /* ---- the hot path ------------------------------------------------------------------------ */
 /* Advance `turns` generations (Broker.Publish called `turns` times, gol/distributor.go:48-49).
  * alive_per_turn (nullable, len turns): alive cells after each completed turn, counted inside the
@@ -140,9 +153,25 @@ int golhip_alive_count(golhip_t h, uint64_t *out);
 /* Alive cells of the handle's rows as (x, y) int32 pairs, row-major (gol/distributor.go:153-166).
  * If the count exceeds cap, returns GOLHIP_ERR_CAP with *n = required count. */
 int golhip_alive_cells(golhip_t h, int32_t *xy, size_t cap, size_t *n);
-/* Cells that changed in the last generation (valid after a step whose last launch advanced 1
- * generation; gol/distributor.go:53-59), (x, y) pairs, row-major; GOLHIP_ERR_STATE otherwise. */
+/* Cells that changed in the last generation (gol/distributor.go:53-59), (x, y) pairs, row-major.
+ * Valid after any golhip_step when flips tracking is on (the step's last launch writes them
+ * beside its output), or after a step whose last launch advanced 1 generation; GOLHIP_ERR_STATE
+ * otherwise. */
 int golhip_flips(golhip_t h, int32_t *xy, size_t cap, size_t *n);
+/* Flips tracking: every golhip_step keeps the flips of its last generation (one extra store per
+ * row in its last launch), so golhip_flips is valid after a K-deep step. */
+int golhip_track_flips(golhip_t h, int enable);
+/* Per-turn CellFlipped for event consumers (the reference's per-turn diff, gol/distributor.go:
+ * 53-59, and TurnComplete, :180-184): advance `turns` generations (<= golhip_flips_ring_capacity)
+ * keeping each turn's flips in a device ring, then return them in ONE extraction: xy = every
+ * turn's flipped cells, turn by turn, row-major within a turn; flips_per_turn[t] (nullable, len
+ * turns) = cells flipped by turn t; alive_per_turn as in golhip_step.  If cap is too small the
+ * turns are still advanced, GOLHIP_ERR_CAP is returned with *n = the required count and
+ * golhip_flips_fetch returns them.  COLLECTIVE like golhip_step. */
+int golhip_step_flips(golhip_t h, int64_t turns, int32_t *xy, size_t cap, size_t *n,
+                      uint64_t *flips_per_turn, uint64_t *alive_per_turn);
+int golhip_flips_ring_capacity(golhip_t h, int64_t *out);
+int golhip_flips_fetch(golhip_t h, int32_t *xy, size_t cap, size_t *n, uint64_t *flips_per_turn);
 /* Completed turns since the last load (the broker's `turn`, broker/broker.go:140). */
 int golhip_turn(golhip_t h, int64_t *out);
 int golhip_set_turn(golhip_t h, int64_t turn);

@@ -4,7 +4,7 @@ gol_stencil template arguments decoded (K, COUNT, SKEW, D, PF, HH, DR, ZIP, FILL
 import re
 import sys
 
-NAMES = ["K", "COUNT", "SKEW", "D", "PF", "HH", "DR", "ZIP", "FILLU"]
+NAMES = ["K", "COUNT", "SKEW", "D", "PF", "HH", "DR", "ZIP", "FILLU", "LD"]
 txt = open(sys.argv[1]).read()
 for b in re.split(r"remark: Function Name: ", txt)[1:]:
     name = b.split()[0]

@@ -87,7 +87,8 @@ static void test_gol(bool pgm) {
                     if (e->kind == EventKind::FinalTurnComplete) {
                         cells = *e->Alive;
                         final_seen = true;
-                        EXPECT(e->CompletedTurns == turns, "final turn %d != %d", e->CompletedTurns, turns);
+                        EXPECT(e->CompletedTurns == turns, "final turn %lld != %d",
+                               (long long)e->CompletedTurns, turns);
                     }
                 }
                 th.join();
@@ -130,9 +131,9 @@ static void test_alive() {
                 expected = e->CompletedTurns == 0 ? 6511 : alive[e->CompletedTurns];
             else
                 expected = e->CompletedTurns % 2 == 0 ? 5565 : 5567;
-            EXPECT(expected == e->CellsCount, "At turn %d expected %d alive cells, got %lld",
-                   e->CompletedTurns, expected, (long long)e->CellsCount);
-            std::printf("Completed Turns %-8d%s\n", e->CompletedTurns, e->String().c_str());
+            EXPECT(expected == e->CellsCount, "At turn %lld expected %d alive cells, got %lld",
+                   (long long)e->CompletedTurns, expected, (long long)e->CellsCount);
+            std::printf("Completed Turns %-8lld%s\n", (long long)e->CompletedTurns, e->String().c_str());
             if (++i >= 5) {
                 keys.send('q');
                 quit_sent = true;
@@ -141,7 +142,7 @@ static void test_alive() {
     }
     th.join();
     EXPECT(i >= 5, "not enough AliveCellsCount events received");
-    reset_saved_state();
+    reset_saved_state(opts());
 }
 
 static void test_sdl() {
@@ -164,7 +165,8 @@ static void test_sdl() {
                 const int count = (int)std::count(board.begin(), board.end(), (uint8_t)255);
                 EXPECT(alive[turn_num] == count, "turn %d: displayed %d alive, should be %d",
                        turn_num, count, alive[turn_num]);
-                EXPECT(e->CompletedTurns == turn_num, "TurnComplete %d != %d", e->CompletedTurns, turn_num);
+                EXPECT(e->CompletedTurns == turn_num, "TurnComplete %lld != %d",
+                       (long long)e->CompletedTurns, turn_num);
                 break;
             }
             case EventKind::FinalTurnComplete: final = true; break;
@@ -197,10 +199,10 @@ static void test_keys() {
         }
         if (e->kind == EventKind::StateChange || e->kind == EventKind::ImageOutputComplete) {
             seen.push_back(*e);
-            std::printf("Completed Turns %-8d%s\n", e->CompletedTurns, e->String().c_str());
+            std::printf("Completed Turns %-8lld%s\n", (long long)e->CompletedTurns, e->String().c_str());
         }
-        if (e->kind == EventKind::ImageOutputComplete) snap_turn = e->CompletedTurns;
-        if (e->kind == EventKind::StateChange && e->NewState == State::Quitting) quit_turn = e->CompletedTurns;
+        if (e->kind == EventKind::ImageOutputComplete) snap_turn = (int)e->CompletedTurns;
+        if (e->kind == EventKind::StateChange && e->NewState == State::Quitting) quit_turn = (int)e->CompletedTurns;
     }
     th.join();
     EXPECT(seen.size() == 4, "expected Paused, snapshot, Executing, Quitting; got %zu", seen.size());
@@ -227,9 +229,9 @@ static void test_keys() {
     int first_turn = -1, final_turn = -1;
     size_t final_cells = 0;
     while (auto e = ev2.recv()) {
-        if (e->kind == EventKind::TurnComplete && first_turn < 0) first_turn = e->CompletedTurns;
+        if (e->kind == EventKind::TurnComplete && first_turn < 0) first_turn = (int)e->CompletedTurns;
         if (e->kind == EventKind::FinalTurnComplete) {
-            final_turn = e->CompletedTurns;
+            final_turn = (int)e->CompletedTurns;
             final_cells = e->Alive->size();
         }
     }

@@ -65,7 +65,9 @@ def test_random_boards_vs_oracle(golhip, oracle, shape, k):
 
 
 def test_flips_match_oracle(golhip, oracle):
-    """CellFlipped per turn (gol/distributor.go:53-59) from the XOR + compaction kernels."""
+    """CellFlipped per turn (gol/distributor.go:53-59) from the XOR + compaction kernels, after
+    one-generation steps and -- with flips tracking -- after k-deep steps (the last launch writes
+    the last generation's flips beside its output)."""
     _, _, board = oracle.read_pgm(REF / "images/512x512.pgm")
     with golhip.Engine(512, 512, k=8) as e:
         e.load(board)
@@ -76,9 +78,96 @@ def test_flips_match_oracle(golhip, oracle):
             got = [tuple(c) for c in e.flips().tolist()]
             assert got == oracle.flips(prev, cur)
             prev = cur
-        e.step(8)
+        e.step(8)  # untracked k-deep step: the previous generation is not held
         with pytest.raises(golhip.GolHipError):
             e.flips()
+        e.track_flips(True)
+        for n in (8, 13, 1, 16):
+            before = e.store()
+            e.step(n)
+            after = e.store()
+            gen_prev, _ = oracle.packed_run(before, n - 1)
+            assert [tuple(c) for c in e.flips().tolist()] == oracle.flips(gen_prev, after), n
+
+
+@pytest.mark.parametrize("variant", ["prod", "driftlds", "drift62"])
+@pytest.mark.parametrize("k", [1, 2, 6, 12, 16, 32])
+@pytest.mark.parametrize("strips", [1, 3])
+def test_tracked_flips_every_depth(golhip, oracle, monkeypatch, variant, k, strips):
+    """Flips tracking at every launch depth, both drift geometries and the multi-strip (halo)
+    path: golhip_flips after a k-deep step == the oracle's diff of the last two generations."""
+    monkeypatch.setenv("GOLHIP_VARIANT", variant)
+    h, w = 111, 4160
+    if h // strips < k:
+        pytest.skip("strip shorter than k")
+    words = oracle.init_random(w, h, seed=k * 10 + strips)
+    with golhip.Engine(w, h, ngpus=1, k=k, strips=strips) as e:
+        e.set_fixed_k(True)
+        e.track_flips(True)
+        e.load_words(words)
+        for n in (k, 2 * k + 1):
+            before = oracle.unpack(e.store_words(), w)
+            e.step(n)
+            after = oracle.unpack(e.store_words(), w)
+            gen_prev, _ = oracle.packed_run(before, n - 1)
+            assert [tuple(c) for c in e.flips().tolist()] == oracle.flips(gen_prev, after), n
+
+
+def test_tracked_flips_small_board_graphs(golhip, oracle, monkeypatch):
+    """Small boards replay captured graphs; with tracking the last launch stays a plain,
+    flips-writing launch."""
+    monkeypatch.setenv("GOLHIP_GRAPHS", "1")
+    _, _, board = oracle.read_pgm(REF / "images/512x512.pgm")
+    gen_prev, _ = oracle.packed_run(board, 299)
+    expected, _ = oracle.packed_run(board, 300)
+    with golhip.Engine(512, 512, k=16) as e:
+        e.track_flips(True)
+        e.load(board)
+        e.step(300)
+        assert np.array_equal(e.store(), expected)
+        assert [tuple(c) for c in e.flips().tolist()] == oracle.flips(gen_prev, expected)
+
+
+@pytest.mark.parametrize("shape,strips", [((512, 512), 1), ((96, 640), 1), ((300, 1000), 2),
+                                          ((130, 4160), 4)])
+def test_step_flips_ring_every_turn(golhip, oracle, shape, strips):
+    """golhip_step_flips: every turn's CellFlipped (turn by turn, row-major) and alive count from
+    ONE extraction over the device ring of per-turn flips boards -- the TestSdl event stream
+    (sdl_test.go:57-74) -- equal to the oracle's per-turn diffs."""
+    h, w = shape
+    rng = np.random.default_rng(h * 3 + w + strips)
+    board = ((rng.random(shape) < 0.4) * 255).astype(np.uint8)
+    with golhip.Engine(w, h, ngpus=1, k=8, strips=strips) as e:
+        e.load(board)
+        assert e.flips_ring_capacity() >= 40
+        prev = oracle.to_cells(board)
+        for turns in (1, 17, 40):
+            per_turn, alive = e.step_flips(turns, counts=True)
+            assert len(per_turn) == turns
+            for t in range(turns):
+                cur, _ = oracle.packed_run(prev, 1)
+                assert [tuple(c) for c in per_turn[t].tolist()] == oracle.flips(prev, cur), (turns, t)
+                assert int(alive[t]) == int((cur == 255).sum())
+                prev = cur
+        assert np.array_equal(e.store(), prev)
+        assert [tuple(c) for c in e.flips().tolist()] == [tuple(c) for c in per_turn[-1].tolist()]
+
+
+def test_step_flips_capacity_errors(golhip, oracle):
+    import ctypes
+
+    _, _, board = oracle.read_pgm(REF / "images/64x64.pgm")
+    with golhip.Engine(64, 64) as e:
+        e.load(board)
+        cap = e.flips_ring_capacity()
+        n = ctypes.c_size_t(0)
+        rc = e._L.golhip_step_flips(e._h, cap + 1, None, 0, ctypes.byref(n), None, None)
+        assert rc == golhip.ERR_ARG
+        rc = e._L.golhip_step_flips(e._h, 3, None, 0, ctypes.byref(n), None, None)
+        assert rc == golhip.ERR_CAP and n.value > 0  # turns advanced; fetch returns the cells
+        buf = np.empty((n.value, 2), np.int32)
+        assert e._L.golhip_flips_fetch(e._h, buf.ctypes.data, n.value, ctypes.byref(n), None) == 0
+        assert e.turn == 3
 
 
 def test_init_random_matches_oracle(golhip, oracle):

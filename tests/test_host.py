@@ -3,6 +3,8 @@ tests (gol_test.go, pgm_test.go, count_test.go, sdl_test.go) restated in tests/h
 here as native binaries."""
 import subprocess
 
+import numpy as np
+
 import pytest
 
 from conftest import PKG, REF
@@ -28,3 +30,102 @@ def test_host_cpu_units(tmp_path):
 def test_reference_integration_tests(name, tmp_path):
     out = run("test_gol_host", name, tmp_path, timeout=240)
     assert f"{name}: ok" in out
+
+
+def settled_turn(t):
+    """A turn with the same 512x512 board as turn t (period 2 from turn 10000 on)."""
+    return t if t <= 10000 else 10000 + (t - 10000) % 2
+
+
+@pytest.mark.gpu
+def test_quit_checkpoint_resumes_in_a_new_process(tmp_path, golhip, oracle):
+    """'q' parks the board in the broker (Pause{P: true, Turn, Dimension}, gol/distributor.go:
+    139-147, broker/broker.go:143-155); a NEW controller process of the same size resumes from it
+    (CheckStates, broker/broker.go:124-141; gol/distributor.go:76-84).  The first process runs
+    the reference's default -turns 10000000000 (> 2^31: Go's 64-bit int, main.go:38-42) and gets
+    'q' after a few ticks; the second resumes for 10 more turns.  The checkpoint board, and the
+    final board, are checked against the oracle and the reference's check/alive/512x512.csv."""
+    import re
+    import time
+
+    gol = LIB / "gol"
+    out = tmp_path / "out"
+    ckpt = tmp_path / "state.ckpt"
+    args = [str(gol), "-w", "512", "-h", "512", "-images", str(REF / "images"), "-out", str(out),
+            "-checkpoint", str(ckpt)]
+    p = subprocess.Popen(args, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+    time.sleep(2.5)  # past the first 2 s tick
+    p.stdin.write("q\n")
+    p.stdin.flush()
+    stdout, _ = p.communicate(timeout=60)
+    assert p.returncode == 0, stdout[-2000:]
+    m = re.search(r"Completed Turns (\d+)\s+Quitting", stdout)
+    assert m, stdout[-2000:]
+    quit_turn = int(m.group(1))
+    assert quit_turn > 0 and "Alive Cells" in stdout
+    w, h, t = golhip.checkpoint_info(ckpt)
+    assert (w, h, t) == (512, 512, quit_turn)
+    # the parked board == the oracle's board after quit_turn turns (the 512x512 board is
+    # period 2 from turn 10000 on: tests/test_oracle.py::test_period_two_tail_board)
+    _, _, board = oracle.read_pgm(REF / "images" / "512x512.pgm")
+    expected, _ = oracle.packed_run(board, settled_turn(quit_turn), threads=1)
+    body = np.frombuffer(ckpt.read_bytes()[64:], dtype=np.uint8).reshape(512, 64)
+    parked = (np.unpackbits(body, axis=1, bitorder="little") * 255).astype(np.uint8)
+    assert np.array_equal(parked, expected)
+    # a new process with the same size resumes at quit_turn and runs to quit_turn + 10
+    p2 = subprocess.run(args[:2] + ["512", "-h", "512", "-turns", str(quit_turn + 10)] + args[5:],
+                        stdin=subprocess.DEVNULL, capture_output=True, text=True, timeout=60)
+    assert p2.returncode == 0, p2.stdout[-2000:]
+    fm = re.search(r"Final turn (\d+): (\d+) alive cells", p2.stdout)
+    assert fm and int(fm.group(1)) == quit_turn + 10, p2.stdout[-2000:]
+    alive = oracle.read_alive_csv(REF / "check" / "alive" / "512x512.csv")
+    tt = quit_turn + 10
+    assert int(fm.group(2)) == (alive[tt] if tt <= 10000 else (5565 if tt % 2 == 0 else 5567))
+    assert not ckpt.exists()  # CheckStates consumed the paused state
+    _, _, last = oracle.read_pgm(out / f"512x512x{tt}.pgm")
+    assert np.array_equal(last, oracle.packed_run(board, settled_turn(tt), threads=1)[0])
+
+
+@pytest.mark.gpu
+def test_checkpoint_other_size_is_discarded(tmp_path, golhip, oracle):
+    """CheckStates with another size does not resume and clears the paused state
+    (broker/broker.go:126-138): a 64x64 run next to a parked 512x512 board starts from turn 0."""
+    _, _, board = oracle.read_pgm(REF / "images" / "512x512.pgm")
+    ckpt = tmp_path / "state.ckpt"
+    with golhip.Engine(512, 512) as e:
+        e.load(board)
+        e.step(7)
+        e.checkpoint_save(ckpt)
+    assert golhip.checkpoint_info(ckpt) == (512, 512, 7)
+    p = subprocess.run([str(LIB / "gol"), "-w", "64", "-h", "64", "-turns", "100", "-images",
+                        str(REF / "images"), "-out", str(tmp_path / "out"), "-checkpoint", str(ckpt)],
+                       stdin=subprocess.DEVNULL, capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stdout[-2000:]
+    assert not ckpt.exists()
+    assert (tmp_path / "out" / "64x64x100.pgm").read_bytes() == (REF / "check" / "images" / "64x64x100.pgm").read_bytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,strips", [((512, 512), 1), ((96, 200), 1), ((300, 1024), 3)])
+def test_checkpoint_roundtrip(tmp_path, golhip, oracle, shape, strips):
+    """golhip_checkpoint_save/load: board and turn restored exactly (widths that are and are not
+    a multiple of 128, multi-strip handles); a mismatched handle is refused."""
+    h, w = shape
+    rng = np.random.default_rng(w + h)
+    board = ((rng.random(shape) < 0.4) * 255).astype(np.uint8)
+    ckpt = tmp_path / "c.ckpt"
+    with golhip.Engine(w, h, ngpus=1, k=8, strips=strips) as e:
+        e.load(board)
+        e.step(21)
+        e.checkpoint_save(ckpt)
+        ref = e.store()
+    assert golhip.checkpoint_info(ckpt) == (w, h, 21)
+    with golhip.Engine(w, h, ngpus=1, k=8, strips=strips) as e:
+        e.checkpoint_load(ckpt)
+        assert e.turn == 21 and np.array_equal(e.store(), ref)
+        e.step(5)
+        assert np.array_equal(e.store(), oracle.packed_run(board, 26)[0])
+    with golhip.Engine(w + 64, h) as e:
+        with pytest.raises(golhip.GolHipError) as ex:
+            e.checkpoint_load(ckpt)
+        assert ex.value.code == golhip.ERR_STATE

@@ -171,3 +171,16 @@ def test_cfg3_golden_prefix_is_the_oracle(oracle):
     w = oracle.init_random(65536, 65536, seed=3)
     counts = oracle.packed_run_words(w, 2)
     assert [int(c) for c in counts] == [expected[1], expected[2]]
+
+
+def test_period_two_tail_board(oracle):
+    """The 512x512 board itself (not only its count, count_test.go:45-51) repeats with period 2
+    from turn 10000: later boards are pinned by turn 10000 or 10001 (tests/test_host.py)."""
+    _, _, b = oracle.read_pgm(REF / "images/512x512.pgm")
+    w = oracle.pack(b)
+    oracle.packed_run_words(w, 10000, threads=1)
+    ref = w.copy()
+    oracle.packed_run_words(w, 1, threads=1)
+    assert not np.array_equal(w, ref)
+    oracle.packed_run_words(w, 1, threads=1)
+    assert np.array_equal(w, ref)
