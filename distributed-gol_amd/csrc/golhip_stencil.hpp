@@ -333,9 +333,12 @@ __device__ __forceinline__ void flush_counts(const uint32_t (&acc)[NL], int j0, 
 //             p.diff: at the last level the mid row's centre cells are generation K-1 in the same
 //             (drifted) frame as the output, so the diff costs one XOR, its realignment and the
 //             store(s) per step.
+// WPE > 0: minimum resident waves per SIMD forced on the register allocator (the vmcnt guard's
+//             self-test instantiates a spilling configuration this way; production: 0).
 template <int K, bool COUNT, bool SKEW, int D, int PF, bool HH, bool DR = false, int ZIP = 1,
-          bool FILLU = true, bool LD = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ZIP == 2 && !COUNT && K >= 12 && K <= 16 ? 4 : 1)))
+          bool FILLU = true, bool LD = false, int WPE = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
+    WPE > 0 ? WPE : (ZIP == 2 && !COUNT && K >= 12 && K <= 16 ? 4 : 1))))
 void gol_stencil(const uint32_t *__restrict__ in,
                                                    uint32_t *__restrict__ out, StencilParams p,
                                                    unsigned long long *__restrict__ slots) {
