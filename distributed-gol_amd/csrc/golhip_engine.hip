@@ -99,6 +99,8 @@ struct golhip_engine {
     bool rank_mode = false;
     bool split = false;  // board held as halo'd row strips (world > 1, or GOLHIP_RING_SELF)
     int force_split = 0;  // GOLHIP_SPLIT (0 = automatic)
+    int force_tile = -1;  // GOLHIP_TILE: -1 automatic, 0 never, T > 0 always (tile height T)
+    int force_slab = -1;  // GOLHIP_SLAB: -1 automatic, 0 never, W*100 + S always (slab shape)
     std::vector<Shard> shards;
     int cur = 0;
     bool prev_valid = false;
@@ -261,6 +263,8 @@ int setup_engine(golhip_t h, int width, int height, int world, int k) {
     if (const char *e = std::getenv("GOLHIP_BAND_ROWS")) h->band_rows = std::atoi(e);
     h->count_window = count_window_env();
     if (const char *e = std::getenv("GOLHIP_SPLIT")) h->force_split = std::atoi(e);
+    if (const char *e = std::getenv("GOLHIP_TILE")) h->force_tile = std::atoi(e);
+    if (const char *e = std::getenv("GOLHIP_SLAB")) h->force_slab = std::atoi(e);
     if (const char *e = std::getenv("GOLHIP_VARIANT"))
         h->variant = std::strcmp(e, "chain") == 0     ? golhip::kVariantChain
                      : std::strcmp(e, "skew") == 0   ? golhip::kVariantSkew
@@ -448,6 +452,56 @@ int pick_split(golhip_t h, int64_t rows_total, int K) {
     return 1;
 }
 
+// The register kernels for boards too small for the streaming kernel (stencil_tile.hip): gol_tile
+// (one wave per T + 2K row tile) and gol_slab (a workgroup of W waves x S rows, edge rows through
+// LDS).  They replace the streaming band's pipeline fill (2K rows per band, one dependency chain
+// per wave) by a K-row trapezoid per tile/slab with every row of a generation independent; they
+// win where the streaming kernel cannot get both tall bands and enough waves (small boards;
+// profiles/r02/tune_tile.txt).
+struct RegKernel {
+    int kind = 0;  // 0 none (streaming), 2 gol_tile, 3 gol_slab
+    int T = 0, W = 0, S = 0;
+    int out_rows() const { return T; }  // output rows per tile / slab
+};
+RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K) {
+    RegKernel rk;
+    if (!golhip::variant_is_production_family(h->variant) || h->split) return rk;
+    // an explicit level split or band height (tests, tuning) asks for the streaming kernels
+    const bool forced = h->force_tile > 0 || h->force_slab > 0;
+    if (!forced && (h->force_split > 0 || h->band_rows > 0)) return rk;
+    // the input descriptor spans the board's rows; offsets are 32-bit signed
+    if ((int64_t)h->height * h->pitch * 4 >= ((int64_t)1 << 31)) return rk;
+    if (h->force_tile > 0) {
+        if (golhip::stencil_tile_supported(K, h->force_tile)) rk.kind = 2, rk.T = h->force_tile;
+        return rk;
+    }
+    if (h->force_slab > 0) {
+        const int W = h->force_slab / 100, S = h->force_slab % 100;
+        if (golhip::stencil_slab_supported(K, W, S)) rk.kind = 3, rk.W = W, rk.S = S, rk.T = W * S - 2 * K;
+        return rk;
+    }
+    if (h->force_tile == 0 || h->force_slab == 0) return rk;
+    // automatic: the slab shape measured best for this depth on small boards, when the streaming
+    // kernel would run short of waves (fewer than two rounds of minimal bands)
+    int W = 16, S = 8;
+    if (!golhip::stencil_slab_supported(K, W, S)) return rk;
+    const int64_t per = golhip::chunk_words(K, h->variant);
+    const int64_t nchunks = (h->wd + per - 1) / per;
+    const int64_t minband = std::max(K, 8);
+    const int64_t waves1 = (rows_total + minband - 1) / minband * nchunks;
+    if (h->cus == 0) {
+        hipDeviceProp_t prop;
+        h->cus = hipGetDeviceProperties(&prop, h->shards[0].device) == hipSuccess
+                     ? prop.multiProcessorCount
+                     : 256;
+    }
+    int &wpc = h->waves_per_cu[K][h->variant];
+    if (wpc == 0) wpc = golhip::stencil_waves_per_cu(K, h->variant);
+    if (waves1 > 2 * (int64_t)h->cus * wpc) return rk;
+    rk.kind = 3, rk.W = W, rk.S = S, rk.T = W * S - 2 * K;
+    return rk;
+}
+
 // Largest band the kernels' 32-bit store offsets can address: a band's output descriptor spans
 // band * rowbytes bytes, and dropped stores use offset kOutOfRange (2^30) + row * rowbytes, so
 // band * rowbytes must stay below 2^30 (golhip_kernels.hip, buffer_store_words).  At 262144 wide
@@ -460,7 +514,18 @@ int64_t max_band_rows(golhip_t h) {
 // Launch the K-generation stencil described by p (level-split kernel when pick_split says so).
 hipError_t launch_auto(golhip_t h, int K, const uint32_t *in, uint32_t *out,
                        const StencilParams &p, unsigned long long *slots, hipStream_t s) {
-    const int S = pick_split(h, (p.r0e - p.r0b) + (p.r1e - p.r1b), K);
+    const int64_t rows_total = (p.r0e - p.r0b) + (p.r1e - p.r1b);
+    if (const RegKernel rk = pick_reg_kernel(h, rows_total, K); rk.kind) {
+        StencilParams q = p;
+        const int T = rk.out_rows();
+        q.band = T;
+        q.nbands0 = (p.r0e - p.r0b + T - 1) / T;
+        q.nbands = q.nbands0 + (p.r1e - p.r1b + T - 1) / T;
+        q.nchunks = (int32_t)((h->wd + golhip::kTileChunkWords - 1) / golhip::kTileChunkWords);
+        return rk.kind == 2 ? golhip::launch_stencil_tile(K, T, in, out, q, slots, s)
+                            : golhip::launch_stencil_slab(K, rk.W, rk.S, in, out, q, slots, s);
+    }
+    const int S = pick_split(h, rows_total, K);
     if (S > 1) {
         // the level-split kernel has its own column geometry (half-word halo for K <= 16)
         StencilParams q = p;
@@ -803,7 +868,11 @@ int create_common(golhip_t h) {
     return GOLHIP_OK;
 }
 
-constexpr int kGraphGens = 128;  // generations per graph replay (<= count_window)
+constexpr int kGraphGens = 128;      // generations per graph replay (<= count_window)
+// Long runs replay larger graphs: each replay of a counting graph ends in a count finalize and a
+// copy of its counts (~17 us together on a 5120^2 board, profiles/r02/small_board_timeline.txt),
+// paid per 1024 generations instead of per 128.
+constexpr int kGraphGensBig = 1024;
 
 // Graphs pay off when a launch is short (launch-bound): < ~100 us of stencil work.
 bool small_board(double cells, int K) { return cells * K <= 8e9; }
@@ -819,22 +888,25 @@ bool graph_worthy(golhip_t h, int K) {
 // next() returns 0 for one graph replay (M x Kfull generations), else one launch's depth.
 struct LaunchPlanner {
     double cells;
-    int Kfull, Kbulk, M;
+    int Kfull, Kbulk, M, Mbig, last_M = 0;
     bool graphs;
     int64_t left;
     bool keep_last;  // the last generation is always a plain launch (it writes the flips)
     LaunchPlanner(double cells_, int k, int64_t turns, bool small, bool fixed = false,
-                  bool keep_last_ = false)
+                  bool keep_last_ = false, int window = 4096)
         : cells(cells_), Kfull(pick_k(k)), left(turns), keep_last(keep_last_) {
         M = std::max(2, (kGraphGens / Kfull) & ~1);
+        Mbig = std::max(M, (std::min(kGraphGensBig, window) / Kfull) & ~1);
         graphs = small && turns >= (int64_t)M * Kfull + (keep_last ? 1 : 0);
         Kbulk = small || fixed ? Kfull : best_rate_k(Kfull);
     }
     int next() {
-        if (graphs && left >= (int64_t)M * Kfull + (keep_last ? 1 : 0)) {
-            left -= (int64_t)M * Kfull;
-            return 0;
-        }
+        for (int m : {Mbig, M})
+            if (graphs && left >= (int64_t)m * Kfull + (keep_last ? 1 : 0)) {
+                left -= (int64_t)m * Kfull;
+                last_M = m;
+                return 0;
+            }
         const int K = left >= 2 * (int64_t)Kbulk ? Kbulk : plan_first_k(left, Kfull, cells);
         left -= K;
         return K;
@@ -851,7 +923,7 @@ int graph_for(golhip_t h, int K, int M, bool counting, hipGraphExec_t *out) {
         }
     HIPCHK(h, hipSetDevice(s.device));
     if (counting && !h->g_counts)
-        HIPCHK(h, hipMalloc(&h->g_counts, sizeof(unsigned long long) * kGraphGens * 2));
+        HIPCHK(h, hipMalloc(&h->g_counts, sizeof(unsigned long long) * kGraphGensBig * 2));
     hipGraph_t graph = nullptr;
     HIPCHK(h, hipStreamBeginCapture(s.compute, hipStreamCaptureModeThreadLocal));
     hipError_t err = hipSuccess;
@@ -1179,12 +1251,14 @@ static int run_steps(golhip_t h, int64_t turns, uint64_t *alive_per_turn, bool r
     }
     int64_t done = 0;
     LaunchPlanner plan((double)h->L * (double)h->height, ring ? 1 : h->k, turns,
-                       !ring && graph_worthy(h, pick_k(h->k)), h->fixed_k || ring, h->track_flips);
-    const int Kfull = plan.Kfull, M = plan.M;
+                       !ring && graph_worthy(h, pick_k(h->k)), h->fixed_k || ring, h->track_flips,
+                       h->count_window);
+    const int Kfull = plan.Kfull;
     int64_t win = 0;  // generations pending in the count window, from turn offset done - win
     while (done < turns) {
         const int K = plan.next();
         if (K == 0) {  // one graph replay of M x Kfull generations
+            const int M = plan.last_M;
             if (counting) {  // the graph finalizes its own generations from window slot 0
                 int rc = flush_counts_window(h, (int)win, done - win);
                 if (rc) return rc;
@@ -1480,6 +1554,22 @@ int golhip_checkpoint_load(golhip_t h, const char *path) {
     return GOLHIP_OK;
 }
 
+int golhip_launch_kind(golhip_t h, int k, int *kind, int *param) {
+    if (!h || !kind || !param || k < 1 || k > golhip::kMaxK) return GOLHIP_ERR_ARG;
+    *kind = 0;
+    *param = 0;
+    if (h->split) return GOLHIP_OK;  // strips: the streaming kernel around the halo exchange
+    const int64_t rows = h->shards[0].rows;
+    if (const RegKernel rk = pick_reg_kernel(h, rows, k); rk.kind) {
+        *kind = rk.kind;
+        *param = rk.kind == 2 ? rk.T : rk.W * 100 + rk.S;
+    } else if (const int S = pick_split(h, rows, k); S > 1) {
+        *kind = 1;
+        *param = S;
+    }
+    return GOLHIP_OK;
+}
+
 int golhip_launch_plan(int64_t width, int64_t height, int strips, int k, int64_t turns,
                        int32_t *depths, size_t cap, size_t *n) {
     if (width <= 0 || height <= 0 || strips <= 0 || k < 1 || k > golhip::kMaxK || turns < 0 || !n)
@@ -1490,7 +1580,7 @@ int golhip_launch_plan(int64_t width, int64_t height, int strips, int k, int64_t
     size_t cnt = 0;
     while (plan.left > 0) {
         const int K = plan.next();
-        if (depths && cnt < cap) depths[cnt] = K == 0 ? -(plan.M * plan.Kfull) : K;
+        if (depths && cnt < cap) depths[cnt] = K == 0 ? -(plan.last_M * plan.Kfull) : K;
         ++cnt;
     }
     *n = cnt;

@@ -113,6 +113,20 @@ hipError_t launch_stencil_split(int K, int S, const uint32_t *in_row0, uint32_t 
                                 const StencilParams &p, unsigned long long *count_slots,
                                 hipStream_t s);
 bool stencil_split_supported(int K, int S);
+// Register-tile stencil (small boards, stencil_tile.hip): each wave holds T + 2K rows of a 62-word
+// column chunk in VGPRs and runs the K generations over them in place; T output rows per wave.
+hipError_t launch_stencil_tile(int K, int T, const uint32_t *in_row0, uint32_t *out_row0,
+                               const StencilParams &p, unsigned long long *count_slots,
+                               hipStream_t s);
+bool stencil_tile_supported(int K, int T);
+// Register slab (stencil_tile.hip): a workgroup of W waves, S rows each, edge rows swapped through
+// LDS every generation; T = W*S - 2K output rows per workgroup.
+hipError_t launch_stencil_slab(int K, int W, int S, const uint32_t *in_row0, uint32_t *out_row0,
+                               const StencilParams &p, unsigned long long *count_slots,
+                               hipStream_t s);
+bool stencil_slab_supported(int K, int W, int S);
+hipError_t warm_stencil_tile(hipStream_t s);
+constexpr int kTileChunkWords = 62;
 // Words per column chunk of the level-split kernel (half-word halo for K <= 16).
 __host__ __device__ constexpr int split_chunk_words(int K) { return K <= 16 ? 63 : 62; }
 // Resident waves per CU of the stencil launch (occupancy query), for sizing the grid.

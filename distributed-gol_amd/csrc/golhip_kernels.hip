@@ -307,6 +307,7 @@ hipError_t warm_stencils(int variant, hipStream_t s) {
     GOLHIP_STENCIL_DEPTHS(GOLHIP_X)
 #undef GOLHIP_X
     if (e == hipSuccess) e = warm_stencil_split(s);
+    if (e == hipSuccess) e = warm_stencil_tile(s);
     return e;
 }
 

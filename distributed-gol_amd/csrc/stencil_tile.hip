@@ -1,0 +1,449 @@
+// stencil_tile.hip -- gol_tile, the register-tile stencil for small boards, and its launchers.
+//
+// Why a second kernel: gol_stencil streams a band of rows through a chain of K generation levels.
+// Each wave is one long dependency chain (row after row, level after level) whose pipeline fill
+// costs 2K rows, so it needs tall bands and many waves.  A small board cannot give it both.  At
+// 5120^2 a K = 16 launch ran 23.7 us, about 12x the VALU time of its useful work
+// (profiles/r02/small_board_timeline.txt): short bands, about one wave per SIMD, and every step
+// waiting on the previous level.
+//
+// gol_tile turns the loop around.  A wave loads a whole tile into VGPRs: R = T + 2K rows of its
+// 64-lane column chunk, the same 62-word chunk geometry as gol_stencil (lanes 0 and 63 are halo).
+// It then runs the K generations over the tile in place.  Generation g recomputes rows
+// [g, R - g): the K-row trapezoid of temporal blocking, with the halo rows going stale from the
+// tile edges inward.  All rows of a generation are independent, so a wave carries R-way ILP
+// instead of one chain.  Finally it stores the T middle rows.  There are no LDS, barriers or
+// pipeline fill.  The cost is the trapezoid: K(R - K - 1) row updates for T useful rows per
+// generation.
+//
+// The row update is gol_stencil's drifting-sum form (row_sum3_drift + life_next): 12 VALU per
+// word per generation (1 DPP, 2 v_alignbit, 9 v_bitop3).  Generation g sits g bits east of the
+// board frame; the stored rows move back with realign_drift<K>.  Counts use the same whole-word
+// window as the 62-word drift geometry.  Rows load through a raw-buffer descriptor with the row
+// offset in an SGPR: one VGPR offset per lane for every row.
+#include "golhip_stencil.hpp"
+
+namespace golhip {
+namespace {
+
+// Independent row chains per wave (segments advanced op-major).
+constexpr int kTileChains = 4;
+
+// Drifting 3-cell sums (row_sum3_drift) of N rows, op-major: each op for every row before the
+// next op, so the N dependency chains interleave.  Rows with use(i) false are skipped.
+struct AllRows {
+    constexpr bool operator()(int) const { return true; }
+};
+template <int N, class U = AllRows>
+__device__ __forceinline__ void sums_om(const uint32_t (&x)[N], uint32_t (&s)[N], uint32_t (&cy)[N],
+                                        uint32_t (&ctr)[N], U use = U{}) {
+    uint32_t wl[N], w2[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        if (use(i)) wl[i] = lane_from_west(x[i]);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        if (use(i)) ctr[i] = __builtin_amdgcn_alignbit(x[i], wl[i], 31);  // cell x-1 onto x
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        if (use(i)) w2[i] = __builtin_amdgcn_alignbit(x[i], wl[i], 30);  // cell x-2 onto x
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        if (use(i)) s[i] = GOL_BOP3(w2[i], ctr[i], x[i], kXor3);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        if (use(i)) cy[i] = GOL_BOP3(w2[i], ctr[i], x[i], kMaj);
+}
+
+// life_next of N rows, op-major (same circuit: 7 v_bitop3 per row).
+template <int N, class U>
+__device__ __forceinline__ void life_om(const uint32_t (&as)[N], const uint32_t (&acy)[N],
+                                        const uint32_t (&ms)[N], const uint32_t (&mcy)[N],
+                                        const uint32_t (&mc)[N], const uint32_t (&bs)[N],
+                                        const uint32_t (&bcy)[N], uint32_t (&out)[N], U use) {
+    uint32_t o[N], k[N], pp[N], q[N], u[N], v[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        if (use(i)) o[i] = GOL_BOP3(as[i], ms[i], bs[i], kXor3);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        if (use(i)) k[i] = GOL_BOP3(as[i], ms[i], bs[i], kMaj);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        if (use(i)) pp[i] = GOL_BOP3(acy[i], mcy[i], bcy[i], kXor3);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        if (use(i)) q[i] = GOL_BOP3(acy[i], mcy[i], bcy[i], kMaj);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        if (use(i)) u[i] = GOL_BOP3(k[i], pp[i], q[i], kTwosEven);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        if (use(i)) v[i] = GOL_BOP3(o[i], q[i], mc[i], kOddSelect);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        if (use(i)) out[i] = GOL_BOP3(v[i], o[i], u[i], GOL_TT(a & (b ^ c)));
+}
+
+// Segment geometry of one generation step i: NS segments over rows [LO, LO + N), segment sg =
+// [first(sg), first(sg + 1)); active: it has a row at step I; fresh: that row's successor needs
+// new sums (not the segment's last row before a next segment, whose first m is saved).
+template <int LO, int N, int NS, int I>
+struct TileStep {
+    static constexpr int first(int sg) { return LO + (N * sg) / NS; }
+    struct Active {
+        constexpr bool operator()(int sg) const { return first(sg) + I < first(sg + 1); }
+    };
+    struct Fresh {
+        constexpr bool operator()(int sg) const {
+            return first(sg) + I < first(sg + 1) && (first(sg) + I + 1 < first(sg + 1) || sg + 1 == NS);
+        }
+    };
+};
+
+// One generation over rows [LO, LO + N) of c (compile time) from the previous generation's rows
+// [LO - 1, LO + N].  The rows are cut into NS segments that advance together, op-major (one op
+// of every segment, then the next op): NS independent dependency chains per wave.  Each segment
+// walks its rows top to bottom holding the sums of the rows above (a), at (m) and below (b) the
+// row; row r is overwritten (WRITE) once its successor's sums are taken, so the update is in
+// place.  Every sum comes from the previous generation: a segment's first a/m are taken before
+// any row is written, and its last row's b is the next segment's first m (saved then).
+// emit(integral_constant<r>, next, centre) sees every new row and the centre cells it replaces
+// (same drifted frame: the last generation's flips are next ^ centre).
+template <int LO, int N, bool WRITE, int R, class F>
+__device__ __forceinline__ void gen_rows(uint32_t (&c)[R], F &&emit) {
+    constexpr int NS = N < kTileChains ? N : kTileChains;
+    using TS0 = TileStep<LO, N, NS, 0>;
+    constexpr int L = (N + NS - 1) / NS;
+    uint32_t as[NS], acy[NS], ms[NS], mcy[NS], mc[NS], ss[NS], scy[NS];
+    {
+        uint32_t x[2 * NS], s2[2 * NS], cy2[2 * NS], c2[2 * NS];
+#pragma unroll
+        for (int sg = 0; sg < NS; ++sg) {
+            x[2 * sg] = c[TS0::first(sg) - 1];
+            x[2 * sg + 1] = c[TS0::first(sg)];
+        }
+        sums_om<2 * NS>(x, s2, cy2, c2);
+#pragma unroll
+        for (int sg = 0; sg < NS; ++sg) {
+            as[sg] = s2[2 * sg], acy[sg] = cy2[2 * sg];
+            ms[sg] = ss[sg] = s2[2 * sg + 1], mcy[sg] = scy[sg] = cy2[2 * sg + 1];
+            mc[sg] = c2[2 * sg + 1];
+        }
+    }
+    static_for(std::make_integer_sequence<int, L>{}, [&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        using TS = TileStep<LO, N, NS, i>;
+        constexpr typename TS::Active active{};
+        constexpr typename TS::Fresh fresh{};
+        uint32_t x[NS], bs[NS], bcy[NS], bc[NS], nx[NS];
+#pragma unroll
+        for (int sg = 0; sg < NS; ++sg) x[sg] = fresh(sg) ? c[TS::first(sg) + i + 1] : 0u;
+        sums_om<NS>(x, bs, bcy, bc, fresh);
+#pragma unroll
+        for (int sg = 0; sg < NS; ++sg)
+            if (active(sg) && !fresh(sg)) bs[sg] = ss[sg + 1], bcy[sg] = scy[sg + 1], bc[sg] = 0u;
+        life_om<NS>(as, acy, ms, mcy, mc, bs, bcy, nx, active);
+        static_for(std::make_integer_sequence<int, NS>{}, [&](auto sgc) {
+            constexpr int sg = decltype(sgc)::value;
+            if constexpr (active(sg)) {
+                constexpr int r = TS::first(sg) + i;
+                emit(std::integral_constant<int, r>{}, nx[sg], mc[sg]);
+                if constexpr (WRITE) c[r] = nx[sg];
+                as[sg] = ms[sg], acy[sg] = mcy[sg];
+                ms[sg] = bs[sg], mcy[sg] = bcy[sg], mc[sg] = bc[sg];
+            }
+        });
+    });
+}
+
+// Input rows through one raw-buffer descriptor over the rows the stream can address (the torus
+// [0, wrap) or the halo'd strip [lo, hi)); the row offset goes in soffset (SGPR), the column in
+// voffset.  Loads c[first .. first + n) from stream row `row0` on.
+template <int FIRST, int NROWS, int R>
+__device__ __forceinline__ void load_rows(uint32_t (&c)[R], const uint32_t *in, const StencilParams &p,
+                                          int row0, int col) {
+    const int rowbytes = (int)(p.pitch * 4);
+    const int base_row = p.wrap_rows > 0 ? 0 : (int)p.lo;
+    const int span_rows = p.wrap_rows > 0 ? (int)p.wrap_rows : (int)(p.hi - p.lo);
+    const __amdgpu_buffer_rsrc_t irsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint32_t *>(in + (int64_t)base_row * p.pitch), 0, span_rows * rowbytes,
+        kBufferRsrcWord3);
+    RowStream rows(p, row0);
+    const int voff = col * 4;
+#pragma unroll
+    for (int r = 0; r < NROWS; ++r) {
+        c[FIRST + r] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(irsrc, voff,
+                                                                      (rows.ly - base_row) * rowbytes, 0);
+        rows.advance();
+    }
+}
+
+template <int K, int T, bool COUNT, bool LD>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) void gol_tile(
+    const uint32_t *__restrict__ in, uint32_t *__restrict__ out, StencilParams p,
+    unsigned long long *__restrict__ slots) {
+    constexpr int R = T + 2 * K;  // tile rows: T output rows with K halo rows above and below
+    static_assert(T >= 1 && K >= 2 && K <= 32, "tile geometry");
+    const int lane = threadIdx.x & 63;
+    const int64_t wave =
+        (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int64_t chunk = wave % p.nchunks;
+    const int64_t bandi = wave / p.nchunks;
+    if (bandi >= p.nbands) return;  // wave-uniform
+    int ya, yb;
+    band_rows(p, bandi, ya, yb);  // yb - ya <= T (the host sets p.band = T)
+    const int nrows = yb - ya;
+    const int colraw = (int)chunk * kTileChunkWords + lane - 1;
+    const int col = (colraw + p.wd) % p.wd;
+    const int rowbytes = (int)(p.pitch * 4);
+    // per-generation counts parked per lane in LDS (runtime generation index), reduced at the end
+    __shared__ uint32_t cnt_lds[4][COUNT ? K : 1][64];
+    const int wl = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    uint32_t c[R];
+    load_rows<0, R>(c, in, p, ya - K, col);
+    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+        out + (int64_t)ya * p.pitch, 0, nrows * rowbytes, kBufferRsrcWord3);
+    __amdgpu_buffer_rsrc_t drsrc = orsrc;
+    if constexpr (LD)
+        drsrc = __builtin_amdgcn_make_buffer_rsrc(p.diff + (int64_t)ya * p.pitch, 0,
+                                                  nrows * rowbytes, kBufferRsrcWord3);
+    const LaneStore ls = lane_store<false>(lane, colraw, col, p.wd);
+    // the 62-word drift count window: lanes 2..63 with colraw <= wd (gol_stencil, count_lane)
+    const bool count_lane = lane >= 2 && colraw <= p.wd;
+
+    // generation `gen` (0-based) over rows [LO, LO + N); LAST: the output rows, stored
+    auto pass = [&](auto lo_c, auto n_c, auto last_c, int gen) {
+        constexpr int LO = decltype(lo_c)::value, N = decltype(n_c)::value;
+        constexpr bool LAST = decltype(last_c)::value;
+        uint32_t cnt = 0;
+        gen_rows<LO, N, !LAST>(c, [&](auto rc, uint32_t nx, uint32_t centre) {
+            constexpr int r = decltype(rc)::value;
+            constexpr bool out_row = r >= K && r < K + T;
+            // rows past the band's end (a short last band) are not the band's
+            const bool mine = out_row && r - K < nrows;
+            if (COUNT && out_row) cnt += __builtin_popcount(mine ? nx : 0u);
+            if constexpr (LAST && out_row) {
+                const int rowoff = mine ? (r - K) * rowbytes : kOutOfRange;
+                Words<1> v;
+                v.w[0] = realign_drift<K>(nx);
+                golhip::store_row<1, false>(orsrc, ls, v, rowoff);
+                if constexpr (LD) {  // the last generation's flips, same (drifted) frame
+                    Words<1> dv;
+                    dv.w[0] = realign_drift<K>(nx ^ centre);
+                    golhip::store_row<1, false>(drsrc, ls, dv, rowoff);
+                }
+            }
+        });
+        if constexpr (COUNT) cnt_lds[wl][gen][lane] = count_lane ? cnt : 0u;
+    };
+    // Generation g (1..K) must produce rows [g, R - g).  The generations run as a loop (one
+    // generation's code is reused from the instruction cache), in two phases of fixed row ranges:
+    // generations 1..H over [1, R - 1), H+1..K-1 over [H+1, R-H-1) (garbage rows outside
+    // [g, R - g) are harmless: they were garbage already), then the last generation over the T
+    // output rows, with the stores.
+    constexpr int H = K / 2;
+    using One = std::integral_constant<int, 1>;
+    using No = std::false_type;
+#pragma clang loop unroll(disable)
+    for (int g = 1; g <= H; ++g) pass(One{}, std::integral_constant<int, R - 2>{}, No{}, g - 1);
+    if constexpr (K - 1 > H) {
+#pragma clang loop unroll(disable)
+        for (int g = H + 1; g <= K - 1; ++g)
+            pass(std::integral_constant<int, H + 1>{}, std::integral_constant<int, R - 2 * (H + 1)>{}, No{},
+                 g - 1);
+    }
+    pass(std::integral_constant<int, K>{}, std::integral_constant<int, T>{}, std::true_type{}, K - 1);
+    if constexpr (COUNT) {
+        uint32_t acc[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) acc[j] = cnt_lds[wl][j][lane];
+        flush_counts<K>(acc, 0, lane, wave, slots);
+    }
+}
+
+// gol_slab: the register tile spread over the W waves of a workgroup.  Wave w holds S rows of the
+// slab's W*S (a 62-word column chunk, rows ya - K + wS ...) in c[1..S]; each generation the waves
+// swap their edge rows through LDS (c[0] = the row above, c[S+1] = the row below, double-buffered
+// by generation parity: one barrier per generation) and update their S rows.  The trapezoid is
+// paid once per slab (2K rows of W*S) instead of once per wave, with S-row waves: more waves per
+// SIMD at the same work.  Output: the T = W*S - 2K middle rows.
+template <int K, int W, int S, bool COUNT, bool LD>
+__global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ in,
+                                                   uint32_t *__restrict__ out, StencilParams p,
+                                                   unsigned long long *__restrict__ slots) {
+    constexpr int T = W * S - 2 * K;
+    static_assert(T >= 1 && K >= 2 && K <= 32 && W >= 2, "slab geometry");
+    __shared__ uint32_t ex[2][W][2][64];
+    // per-generation alive counts of the slab, per lane (summed over the waves by LDS adds; one
+    // global atomic per generation per slab at the end)
+    __shared__ uint32_t cnt_lds[COUNT ? K : 1][64];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int64_t group = blockIdx.x;
+    const int64_t chunk = group % p.nchunks;
+    const int64_t bandi = group / p.nchunks;
+    if (bandi >= p.nbands) return;  // whole workgroup
+    int ya, yb;
+    band_rows(p, bandi, ya, yb);  // yb - ya <= T (the host sets p.band = T)
+    const int nrows = yb - ya;
+    const int colraw = (int)chunk * kTileChunkWords + lane - 1;
+    const int col = (colraw + p.wd) % p.wd;
+    const int rowbytes = (int)(p.pitch * 4);
+    uint32_t c[S + 2];
+    c[0] = c[S + 1] = 0;
+    load_rows<1, S>(c, in, p, ya - K + w * S, col);
+    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+        out + (int64_t)ya * p.pitch, 0, nrows * rowbytes, kBufferRsrcWord3);
+    __amdgpu_buffer_rsrc_t drsrc = orsrc;
+    if constexpr (LD)
+        drsrc = __builtin_amdgcn_make_buffer_rsrc(p.diff + (int64_t)ya * p.pitch, 0,
+                                                  nrows * rowbytes, kBufferRsrcWord3);
+    const LaneStore ls = lane_store<false>(lane, colraw, col, p.wd);
+    const bool count_lane = lane >= 2 && colraw <= p.wd;
+    // slab row of c[1]: output row o = w*S + (r - 1) - K is this band's if 0 <= o < nrows
+    const int o0 = w * S - K;
+    if constexpr (COUNT)
+        for (int j = w; j < K; j += W) cnt_lds[j][lane] = 0;
+    // LDS-only barrier: the waves' global stores and count atomics stay in flight (a
+    // __syncthreads() would also drain vmcnt every generation)
+    auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    auto exchange = [&](int g) {
+        const int par = g & 1;
+        ex[par][w][0][lane] = c[1];
+        ex[par][w][1][lane] = c[S];
+        lds_barrier();
+        c[0] = w > 0 ? ex[par][w - 1][1][lane] : 0u;
+        c[S + 1] = w < W - 1 ? ex[par][w + 1][0][lane] : 0u;
+    };
+    auto pass = [&](auto last_c, int gen) {
+        constexpr bool LAST = decltype(last_c)::value;
+        uint32_t cnt = 0;
+        gen_rows<1, S, !LAST>(c, [&](auto rc, uint32_t nx, uint32_t centre) {
+            constexpr int r = decltype(rc)::value;
+            const int o = o0 + r - 1;
+            const bool mine = o >= 0 && o < nrows;  // wave-uniform
+            if (COUNT) cnt += __builtin_popcount(mine ? nx : 0u);
+            if constexpr (LAST) {
+                const int rowoff = mine ? o * rowbytes : kOutOfRange;
+                Words<1> v;
+                v.w[0] = realign_drift<K>(nx);
+                golhip::store_row<1, false>(orsrc, ls, v, rowoff);
+                if constexpr (LD) {
+                    Words<1> dv;
+                    dv.w[0] = realign_drift<K>(nx ^ centre);
+                    golhip::store_row<1, false>(drsrc, ls, dv, rowoff);
+                }
+            }
+        });
+        if constexpr (COUNT)
+            if (count_lane) __hip_atomic_fetch_add(&cnt_lds[gen][lane], cnt, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+#pragma clang loop unroll(disable)
+    for (int g = 1; g < K; ++g) {
+        exchange(g);
+        pass(std::false_type{}, g - 1);
+    }
+    exchange(K);
+    pass(std::true_type{}, K - 1);
+    if constexpr (COUNT) {
+        lds_barrier();
+        for (int j = w; j < K; j += W) {
+            uint32_t acc[1] = {cnt_lds[j][lane]};
+            flush_counts<1>(acc, j, lane, group, slots);
+        }
+    }
+}
+
+template <int K, int T>
+hipError_t launch_tile_kt(const uint32_t *in, uint32_t *out, const StencilParams &p,
+                          unsigned long long *slots, hipStream_t s) {
+    const int64_t waves = p.nbands * (int64_t)p.nchunks;
+    const unsigned blocks = (unsigned)std::max<int64_t>(1, (waves + 3) / 4);
+    if (p.diff) {
+        if (slots)
+            hipLaunchKernelGGL((gol_tile<K, T, true, true>), dim3(blocks), dim3(256), 0, s, in, out, p, slots);
+        else
+            hipLaunchKernelGGL((gol_tile<K, T, false, true>), dim3(blocks), dim3(256), 0, s, in, out, p, slots);
+    } else if (slots) {
+        hipLaunchKernelGGL((gol_tile<K, T, true, false>), dim3(blocks), dim3(256), 0, s, in, out, p, slots);
+    } else {
+        hipLaunchKernelGGL((gol_tile<K, T, false, false>), dim3(blocks), dim3(256), 0, s, in, out, p, slots);
+    }
+    return hipGetLastError();
+}
+
+template <int K, int W, int S>
+hipError_t launch_slab_kws(const uint32_t *in, uint32_t *out, const StencilParams &p,
+                           unsigned long long *slots, hipStream_t s) {
+    const unsigned blocks = (unsigned)std::max<int64_t>(1, p.nbands * (int64_t)p.nchunks);
+    const dim3 block(64 * W);
+    if (p.diff) {
+        if (slots)
+            hipLaunchKernelGGL((gol_slab<K, W, S, true, true>), dim3(blocks), block, 0, s, in, out, p, slots);
+        else
+            hipLaunchKernelGGL((gol_slab<K, W, S, false, true>), dim3(blocks), block, 0, s, in, out, p, slots);
+    } else if (slots) {
+        hipLaunchKernelGGL((gol_slab<K, W, S, true, false>), dim3(blocks), block, 0, s, in, out, p, slots);
+    } else {
+        hipLaunchKernelGGL((gol_slab<K, W, S, false, false>), dim3(blocks), block, 0, s, in, out, p, slots);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace
+
+#define GOLHIP_SLAB_CONFIGS(X) \
+    X(8, 8, 4) X(8, 8, 8) X(8, 16, 4) X(8, 16, 8) X(12, 8, 8) X(12, 16, 4) X(12, 16, 8) \
+    X(16, 8, 8) X(16, 8, 16) X(16, 16, 4) X(16, 16, 8) X(16, 16, 16)
+
+bool stencil_slab_supported(int K, int W, int S) {
+#define GOLHIP_X(KK, WW, SS) \
+    if (K == KK && W == WW && S == SS) return true;
+    GOLHIP_SLAB_CONFIGS(GOLHIP_X)
+#undef GOLHIP_X
+    return false;
+}
+
+hipError_t launch_stencil_slab(int K, int W, int S, const uint32_t *in_row0, uint32_t *out_row0,
+                               const StencilParams &p, unsigned long long *slots, hipStream_t s) {
+#define GOLHIP_X(KK, WW, SS) \
+    if (K == KK && W == WW && S == SS) return launch_slab_kws<KK, WW, SS>(in_row0, out_row0, p, slots, s);
+    GOLHIP_SLAB_CONFIGS(GOLHIP_X)
+#undef GOLHIP_X
+    return hipErrorInvalidValue;
+}
+
+#define GOLHIP_TILE_CONFIGS(X) \
+    X(2, 16) X(4, 8) X(4, 16) X(4, 32) X(6, 16) X(8, 8) X(8, 16) X(8, 32) X(10, 16) X(12, 8) \
+    X(12, 16) X(12, 32) X(14, 16) X(16, 8) X(16, 16) X(16, 32)
+
+bool stencil_tile_supported(int K, int T) {
+#define GOLHIP_X(KK, TT) \
+    if (K == KK && T == TT) return true;
+    GOLHIP_TILE_CONFIGS(GOLHIP_X)
+#undef GOLHIP_X
+    return false;
+}
+
+hipError_t launch_stencil_tile(int K, int T, const uint32_t *in_row0, uint32_t *out_row0,
+                               const StencilParams &p, unsigned long long *slots, hipStream_t s) {
+#define GOLHIP_X(KK, TT) \
+    if (K == KK && T == TT) return launch_tile_kt<KK, TT>(in_row0, out_row0, p, slots, s);
+    GOLHIP_TILE_CONFIGS(GOLHIP_X)
+#undef GOLHIP_X
+    return hipErrorInvalidValue;
+}
+
+hipError_t warm_stencil_tile(hipStream_t s) {
+    StencilParams p{};
+    p.nchunks = 1;  // nbands = 0: every wave returns at once
+    hipLaunchKernelGGL((gol_tile<16, 16, false, false>), dim3(1), dim3(256), 0, s, nullptr, nullptr, p,
+                       nullptr);
+    hipLaunchKernelGGL((gol_slab<16, 16, 8, false, false>), dim3(1), dim3(1024), 0, s, nullptr, nullptr, p,
+                       nullptr);
+    return hipGetLastError();
+}
+
+}  // namespace golhip

@@ -6,6 +6,8 @@ FETCH_SIZE under-counts wide streaming reads by 2x and other widths are uncalibr
 and write scales are CALIBRATED here on two kernels of known traffic that use the stencil's own
 access width (4-byte lanes): popcount_rows reads exactly the board once, init_random_rows writes
 exactly the board once.
+valu_instr_per_launch: SQ_INSTS_VALU of one stencil dispatch (wave64 instructions issued);
+clock_ghz: GRBM_GUI_ACTIVE / 8 / the dispatch duration of the same pass's --kernel-trace.
 Usage: pmc_summary.py <pmc dir> <k> <board bytes> [<json out> <key>]
 """
 import csv
@@ -13,6 +15,7 @@ import glob
 import json
 import sys
 from collections import defaultdict
+from pathlib import Path
 
 
 def load(d):
@@ -22,13 +25,36 @@ def load(d):
     return rows
 
 
+def short_name(name):
+    return ("stencil" if ("gol_stencil" in name or "gol_step1" in name) else "popcount" if "popcount_rows" in name
+            else "init" if "init_random" in name else None)
+
+
+def grbm_clock(d):
+    """Effective clock of the stencil dispatches: GRBM_GUI_ACTIVE (summed over the 8 XCDs) / 8 /
+    the dispatch's duration from the same run's --kernel-trace (MI355X_MICROARCH.md, DVFS)."""
+    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        grbm = {r["Dispatch_Id"]: float(r["Counter_Value"]) for r in csv.DictReader(open(f))
+                if r["Counter_Name"] == "GRBM_GUI_ACTIVE" and short_name(r.get("Kernel_Name", "")) == "stencil"}
+        if not grbm:
+            continue
+        ghz, durs = [], []
+        for t in glob.glob(f"{Path(f).parent}/*kernel_trace.csv"):
+            for r in csv.DictReader(open(t)):
+                if r["Dispatch_Id"] in grbm:
+                    ns = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+                    durs.append(ns)
+                    ghz.append(grbm[r["Dispatch_Id"]] / 8 / ns)
+        if ghz:
+            return sum(ghz) / len(ghz), sum(durs) / len(durs)
+    return None, None
+
+
 def main():
     d, k, board = sys.argv[1], int(sys.argv[2]), float(sys.argv[3])
     per = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> values per dispatch
     for r in load(d):
-        name = r.get("Kernel_Name", "")
-        short = ("stencil" if ("gol_stencil" in name or "gol_step1" in name) else "popcount" if "popcount_rows" in name
-                 else "init" if "init_random" in name else None)
+        short = short_name(r.get("Kernel_Name", ""))
         if short:
             per[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
     avg = {kn: {c: sum(v) / len(v) for c, v in cs.items()} for kn, cs in per.items()}
@@ -45,6 +71,12 @@ def main():
     except KeyError as e:
         out["error"] = f"missing {e}"
     st = avg.get("stencil", {})
+    if "SQ_INSTS_VALU" in st:
+        out["valu_instr_per_launch"] = st["SQ_INSTS_VALU"]
+    clock, dur = grbm_clock(d)
+    if clock:
+        out["clock_ghz"] = round(clock, 3)
+        out["kernel_trace_avg_ns_grbm_pass"] = round(dur)
     if "SQ_LDS_BANK_CONFLICT" in st and st.get("SQ_LDS_IDX_ACTIVE"):
         # extra LDS cycles from bank conflicts over all LDS-array cycles (MI355X_MICROARCH.md)
         out["lds_bank_conflict_cycles"] = st["SQ_LDS_BANK_CONFLICT"]

@@ -99,3 +99,12 @@ def test_launch_plan_small_boards_replay_graphs(golhip):
     assert graphs and sum(graphs) + sum(d for d in plan if d > 0) == 1000000
     assert not any(d < 0 for d in golhip.launch_plan(65536, 65536, 16, 1000))
     assert not any(d < 0 for d in golhip.launch_plan(4096, 4096, 16, 1000000, strips=2))
+
+
+def test_launch_plan_long_runs_replay_large_graphs(golhip):
+    """Long small-board runs replay 1024-generation graphs (one count finalize + copy per replay),
+    then 128-generation graphs, then single launches."""
+    plan = golhip.launch_plan(5120, 5120, 16, 10000)
+    graphs = [-d for d in plan if d < 0]
+    assert graphs[:9] == [1024] * 9 and set(graphs[9:]) <= {128}
+    assert sum(graphs) + sum(d for d in plan if d > 0) == 10000

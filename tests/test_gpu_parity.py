@@ -383,3 +383,99 @@ def test_count_window_flushes(golhip, oracle, monkeypatch, k):
     exp, exp_counts = oracle.packed_run(board, 700)
     assert np.array_equal(got, exp)
     assert np.array_equal(c.astype(np.int64), exp_counts)  # exp_counts[i]: after turn i + 1
+
+
+TILE_CONFIGS = [(2, 16), (4, 8), (4, 16), (4, 32), (6, 16), (8, 8), (8, 16), (8, 32), (10, 16),
+                (12, 8), (12, 16), (12, 32), (14, 16), (16, 8), (16, 16), (16, 32)]
+
+
+@pytest.mark.parametrize("k,tile", TILE_CONFIGS)
+def test_register_tile_kernel(golhip, oracle, monkeypatch, k, tile):
+    """The register-tile stencil (gol_tile: T + 2K rows of a 62-word chunk in VGPRs, K
+    generations in place) forced at every compiled (K, T): wrap in both directions, boards
+    shorter than a tile and than its halo, ragged widths, short last tiles, per-turn counts."""
+    monkeypatch.setenv("GOLHIP_TILE", str(tile))
+    for (h, w) in [(77, 640), (16, 16), (5, 96), (300, 4160), (129, 200), (40, 8192), (64, 1984)]:
+        rng = np.random.default_rng(h * 7 + w + k + tile)
+        board = ((rng.random((h, w)) < 0.4) * 255).astype(np.uint8)
+        turns = 3 * k + 1
+        exp, exp_counts = oracle.packed_run(board, turns)
+        out, counts, _, _ = run_engine(golhip, board, turns, k=k, counts=True)
+        assert np.array_equal(out, exp), (k, tile, h, w)
+        assert np.array_equal(counts.astype(np.int64), exp_counts), (k, tile, h, w)
+
+
+@pytest.mark.parametrize("k", [4, 16])
+def test_register_tile_tracked_flips(golhip, oracle, monkeypatch, k):
+    """Flips tracking through the tile kernel: the last launch's LD instantiation writes the last
+    generation's flips beside its output."""
+    monkeypatch.setenv("GOLHIP_TILE", "16")
+    h, w = 300, 640
+    rng = np.random.default_rng(k)
+    board = ((rng.random((h, w)) < 0.4) * 255).astype(np.uint8)
+    turns = 2 * k + 1
+    before, _ = oracle.packed_run(board, turns - 1)
+    exp, _ = oracle.packed_run(board, turns)
+    with golhip.Engine(w, h, k=k) as e:
+        e.set_fixed_k(True)
+        e.track_flips(True)
+        e.load(board)
+        e.step(turns)
+        assert e.launch_kind(k) == ("tile", 16)
+        got = [tuple(c) for c in e.flips().tolist()]
+        assert np.array_equal(e.store(), exp)
+    assert got == oracle.flips(before, exp)
+
+
+SLAB_CONFIGS = [(8, 8, 4), (8, 8, 8), (8, 16, 4), (8, 16, 8), (12, 8, 8), (12, 16, 4), (12, 16, 8),
+                (16, 8, 8), (16, 8, 16), (16, 16, 4), (16, 16, 8), (16, 16, 16)]
+
+
+@pytest.mark.parametrize("k,waves,rows", SLAB_CONFIGS)
+def test_register_slab_kernel(golhip, oracle, monkeypatch, k, waves, rows):
+    """The register-slab stencil (gol_slab: W waves x S rows of a 62-word chunk in VGPRs, edge
+    rows swapped through LDS every generation) forced at every compiled (K, W, S): wrap, boards
+    shorter than a slab, ragged widths, short last slabs, per-turn counts."""
+    monkeypatch.setenv("GOLHIP_SLAB", str(waves * 100 + rows))
+    for (h, w) in [(77, 640), (16, 16), (5, 96), (300, 4160), (129, 200), (40, 8192), (250, 1984)]:
+        rng = np.random.default_rng(h * 7 + w + k + waves + rows)
+        board = ((rng.random((h, w)) < 0.4) * 255).astype(np.uint8)
+        turns = 3 * k + 1
+        exp, exp_counts = oracle.packed_run(board, turns)
+        with golhip.Engine(w, h, k=k) as e:
+            assert e.launch_kind(k) == ("slab", waves * 100 + rows)
+        out, counts, _, _ = run_engine(golhip, board, turns, k=k, counts=True)
+        assert np.array_equal(out, exp), (k, waves, rows, h, w)
+        assert np.array_equal(counts.astype(np.int64), exp_counts), (k, waves, rows, h, w)
+
+
+def test_register_slab_tracked_flips(golhip, oracle, monkeypatch):
+    monkeypatch.setenv("GOLHIP_SLAB", "1608")
+    h, w, k = 300, 640, 16
+    rng = np.random.default_rng(5)
+    board = ((rng.random((h, w)) < 0.4) * 255).astype(np.uint8)
+    turns = 2 * k + 1
+    before, _ = oracle.packed_run(board, turns - 1)
+    exp, _ = oracle.packed_run(board, turns)
+    with golhip.Engine(w, h, k=k) as e:
+        e.set_fixed_k(True)
+        e.track_flips(True)
+        e.load(board)
+        e.step(turns)
+        got = [tuple(c) for c in e.flips().tolist()]
+        assert np.array_equal(e.store(), exp)
+    assert got == oracle.flips(before, exp)
+
+
+def test_small_board_picks_register_slab(golhip, oracle):
+    """configs[1]-sized boards take the register-slab path automatically (with the planner's own
+    depth choice); results unchanged, counts every turn."""
+    words = oracle.init_random(5120, 512, seed=2)
+    with golhip.Engine(5120, 512, k=16) as e:
+        assert e.launch_kind(16) == ("slab", 1608)
+        e.load_words(words)
+        counts = e.step(200, counts=True)
+        got = e.store_words()
+    ref_counts = oracle.packed_run_words(words, 200)
+    assert np.array_equal(got, words)
+    assert np.array_equal(counts.astype(np.int64), ref_counts)
