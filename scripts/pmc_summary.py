@@ -31,20 +31,21 @@ def short_name(name):
 
 
 def grbm_clock(d):
-    """Effective clock of the stencil dispatches: GRBM_GUI_ACTIVE (summed over the 8 XCDs) / 8 /
-    the dispatch's duration from the same run's --kernel-trace (MI355X_MICROARCH.md, DVFS)."""
+    """Effective clock of the timed stencil dispatches (largest grid): GRBM_GUI_ACTIVE (summed
+    over the 8 XCDs) / 8 / the dispatch's duration (MI355X_MICROARCH.md, DVFS give-back)."""
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
-        grbm = {r["Dispatch_Id"]: float(r["Counter_Value"]) for r in csv.DictReader(open(f))
-                if r["Counter_Name"] == "GRBM_GUI_ACTIVE" and short_name(r.get("Kernel_Name", "")) == "stencil"}
-        if not grbm:
+        rows = [r for r in csv.DictReader(open(f))
+                if r["Counter_Name"] == "GRBM_GUI_ACTIVE" and short_name(r.get("Kernel_Name", "")) == "stencil"]
+        if not rows:
             continue
+        big = max(int(r["Grid_Size"]) for r in rows)
         ghz, durs = [], []
-        for t in glob.glob(f"{Path(f).parent}/*kernel_trace.csv"):
-            for r in csv.DictReader(open(t)):
-                if r["Dispatch_Id"] in grbm:
-                    ns = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-                    durs.append(ns)
-                    ghz.append(grbm[r["Dispatch_Id"]] / 8 / ns)
+        for r in rows:
+            if int(r["Grid_Size"]) != big:
+                continue
+            ns = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            durs.append(ns)
+            ghz.append(float(r["Counter_Value"]) / 8 / ns)
         if ghz:
             return sum(ghz) / len(ghz), sum(durs) / len(durs)
     return None, None
@@ -53,8 +54,14 @@ def grbm_clock(d):
 def main():
     d, k, board = sys.argv[1], int(sys.argv[2]), float(sys.argv[3])
     per = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> values per dispatch
-    for r in load(d):
+    rows = load(d)
+    # the timed stencil launches only: the largest grid (the engine also launches every depth's
+    # kernel once, empty, to load its code object at create)
+    big = max((int(r["Grid_Size"]) for r in rows if short_name(r.get("Kernel_Name", "")) == "stencil"), default=0)
+    for r in rows:
         short = short_name(r.get("Kernel_Name", ""))
+        if short == "stencil" and int(r["Grid_Size"]) != big:
+            continue
         if short:
             per[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
     avg = {kn: {c: sum(v) / len(v) for c, v in cs.items()} for kn, cs in per.items()}
