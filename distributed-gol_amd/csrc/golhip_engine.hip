@@ -481,9 +481,12 @@ RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K) {
         return rk;
     }
     if (h->force_tile == 0 || h->force_slab == 0) return rk;
-    // automatic: the slab shape measured best for this depth on small boards, when the streaming
-    // kernel would run short of waves (fewer than two rounds of minimal bands)
-    int W = 16, S = 8;
+    // automatic: the slab shape measured best for this depth (profiles/r02/small_boards.txt: at
+    // K = 16, 8 waves x 12 rows -- 64 output rows per slab, 240 slabs at 5120^2, about one per CU
+    // -- 1.33 us per turn with counts vs 1.62 for the level split, 1.21 vs 1.35 at 4096^2, 2.45
+    // vs 2.87 at 8192^2), on boards where the streaming kernel has fewer than four minimal-band
+    // waves per SIMD
+    int W = 8, S = K == 16 ? 12 : 8;
     if (!golhip::stencil_slab_supported(K, W, S)) return rk;
     const int64_t per = golhip::chunk_words(K, h->variant);
     const int64_t nchunks = (h->wd + per - 1) / per;
@@ -495,9 +498,7 @@ RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K) {
                      ? prop.multiProcessorCount
                      : 256;
     }
-    int &wpc = h->waves_per_cu[K][h->variant];
-    if (wpc == 0) wpc = golhip::stencil_waves_per_cu(K, h->variant);
-    if (waves1 > 2 * (int64_t)h->cus * wpc) return rk;
+    if (waves1 > 16 * (int64_t)h->cus) return rk;
     rk.kind = 3, rk.W = W, rk.S = S, rk.T = W * S - 2 * K;
     return rk;
 }

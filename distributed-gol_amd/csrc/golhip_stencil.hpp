@@ -291,20 +291,33 @@ __device__ __forceinline__ void store_row(__amdgpu_buffer_rsrc_t r, const LaneSt
     }
 }
 
-// Per-level alive counts of a wave -> its spread slot of each generation (agent-scope atomics).
+// Sum of v over the wave's 64 lanes, returned in lane 63: the DPP prefix-sum ladder (row_shr 1, 2,
+// 4, 8 within each 16-lane row, then row_bcast 15 / 31 across rows) -- 6 dependent VALU ops
+// instead of 6 dependent ds_bpermute round trips through the LDS pipe.
+__device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111 /* row_shr:1 */, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112 /* row_shr:2 */, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114 /* row_shr:4 */, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118 /* row_shr:8 */, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142 /* row_bcast:15 */, 0xa, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143 /* row_bcast:31 */, 0xc, 0xf, false);
+    return v;
+}
+
+// Per-level alive counts of a wave -> its spread slot of each generation (agent-scope atomics,
+// issued by lane 63, which holds the wave's sum).
 template <int NL>
 __device__ __forceinline__ void flush_counts(const uint32_t (&acc)[NL], int j0, int lane,
                                              int64_t wave, unsigned long long *slots) {
+    uint32_t v[NL];
 #pragma unroll
-    for (int j = 0; j < NL; ++j) {
-        uint32_t v = acc[j];
+    for (int j = 0; j < NL; ++j) v[j] = wave_sum_dpp(acc[j]);
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-        if (lane == 0 && v)
+    for (int j = 0; j < NL; ++j)
+        if (lane == 63 && v[j])
             __hip_atomic_fetch_add(&slots[(j0 + j) * kCountSlots + (int)(wave & (kCountSlots - 1))],
-                                   (unsigned long long)v, __ATOMIC_RELAXED,
+                                   (unsigned long long)v[j], __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
-    }
 }
 
 // Column geometry of a wave's 64 lanes (shared with the host via chunk_words()):

@@ -316,13 +316,16 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
         c[0] = w > 0 ? ex[par][w - 1][1][lane] : 0u;
         c[S + 1] = w < W - 1 ? ex[par][w + 1][0][lane] : 0u;
     };
-    auto pass = [&](auto last_c, int gen) {
-        constexpr bool LAST = decltype(last_c)::value;
+    // FULL: every row of this wave is an output row of the band (interior waves): the counts need
+    // no per-row mask (one v_bcnt per row instead of a select and a v_bcnt)
+    const bool full = o0 >= 0 && o0 + S <= nrows;
+    auto pass = [&](auto last_c, auto full_c, int gen) {
+        constexpr bool LAST = decltype(last_c)::value, FULL = decltype(full_c)::value;
         uint32_t cnt = 0;
         gen_rows<1, S, !LAST>(c, [&](auto rc, uint32_t nx, uint32_t centre) {
             constexpr int r = decltype(rc)::value;
             const int o = o0 + r - 1;
-            const bool mine = o >= 0 && o < nrows;  // wave-uniform
+            const bool mine = FULL || (o >= 0 && o < nrows);  // wave-uniform
             if (COUNT) cnt += __builtin_popcount(mine ? nx : 0u);
             if constexpr (LAST) {
                 const int rowoff = mine ? o * rowbytes : kOutOfRange;
@@ -340,13 +343,18 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
             if (count_lane) __hip_atomic_fetch_add(&cnt_lds[gen][lane], cnt, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_WORKGROUP);
     };
+    using No = std::false_type;
+    using Yes = std::true_type;
 #pragma clang loop unroll(disable)
     for (int g = 1; g < K; ++g) {
         exchange(g);
-        pass(std::false_type{}, g - 1);
+        if (COUNT && full)
+            pass(No{}, Yes{}, g - 1);
+        else
+            pass(No{}, No{}, g - 1);
     }
     exchange(K);
-    pass(std::true_type{}, K - 1);
+    pass(Yes{}, No{}, K - 1);
     if constexpr (COUNT) {
         lds_barrier();
         for (int j = w; j < K; j += W) {
@@ -396,7 +404,9 @@ hipError_t launch_slab_kws(const uint32_t *in, uint32_t *out, const StencilParam
 
 #define GOLHIP_SLAB_CONFIGS(X) \
     X(8, 8, 4) X(8, 8, 8) X(8, 16, 4) X(8, 16, 8) X(12, 8, 8) X(12, 16, 4) X(12, 16, 8) \
-    X(16, 8, 8) X(16, 8, 16) X(16, 16, 4) X(16, 16, 8) X(16, 16, 16)
+    X(16, 8, 8) X(16, 8, 10) X(16, 8, 11) X(16, 8, 12) X(16, 8, 13) X(16, 8, 14) X(16, 8, 16) \
+    X(16, 8, 20) X(16, 8, 24) X(16, 16, 4) X(16, 16, 6) X(16, 16, 8) X(16, 16, 16) X(16, 4, 16) \
+    X(16, 4, 24)
 
 bool stencil_slab_supported(int K, int W, int S) {
 #define GOLHIP_X(KK, WW, SS) \

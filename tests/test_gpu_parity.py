@@ -428,7 +428,9 @@ def test_register_tile_tracked_flips(golhip, oracle, monkeypatch, k):
 
 
 SLAB_CONFIGS = [(8, 8, 4), (8, 8, 8), (8, 16, 4), (8, 16, 8), (12, 8, 8), (12, 16, 4), (12, 16, 8),
-                (16, 8, 8), (16, 8, 16), (16, 16, 4), (16, 16, 8), (16, 16, 16)]
+                (16, 8, 8), (16, 8, 10), (16, 8, 11), (16, 8, 12), (16, 8, 13), (16, 8, 14), (16, 8, 16),
+                (16, 8, 20), (16, 8, 24), (16, 16, 4), (16, 16, 6), (16, 16, 8), (16, 16, 16), (16, 4, 16),
+                (16, 4, 24)]
 
 
 @pytest.mark.parametrize("k,waves,rows", SLAB_CONFIGS)
@@ -472,7 +474,8 @@ def test_small_board_picks_register_slab(golhip, oracle):
     depth choice); results unchanged, counts every turn."""
     words = oracle.init_random(5120, 512, seed=2)
     with golhip.Engine(5120, 512, k=16) as e:
-        assert e.launch_kind(16) == ("slab", 1608)
+        assert e.launch_kind(16) == ("slab", 812)
+        assert e.launch_kind(8) == ("slab", 808)
         e.load_words(words)
         counts = e.step(200, counts=True)
         got = e.store_words()
