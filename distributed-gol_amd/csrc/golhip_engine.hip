@@ -460,7 +460,7 @@ int pick_split(golhip_t h, int64_t rows_total, int K) {
 // profiles/r02/tune_tile.txt).
 struct RegKernel {
     int kind = 0;  // 0 none (streaming), 2 gol_tile, 3 gol_slab
-    int T = 0, W = 0, S = 0;
+    int T = 0, W = 0, S = 0, NC = 4;
     int out_rows() const { return T; }  // output rows per tile / slab
 };
 RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K) {
@@ -475,9 +475,11 @@ RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K) {
         if (golhip::stencil_tile_supported(K, h->force_tile)) rk.kind = 2, rk.T = h->force_tile;
         return rk;
     }
-    if (h->force_slab > 0) {
-        const int W = h->force_slab / 100, S = h->force_slab % 100;
-        if (golhip::stencil_slab_supported(K, W, S)) rk.kind = 3, rk.W = W, rk.S = S, rk.T = W * S - 2 * K;
+    if (h->force_slab > 0) {  // [NC x 10000 +] W x 100 + S
+        const int NC = h->force_slab >= 10000 ? h->force_slab / 10000 : 4;
+        const int W = h->force_slab / 100 % 100, S = h->force_slab % 100;
+        if (golhip::stencil_slab_supported(K, W, S, NC))
+            rk.kind = 3, rk.W = W, rk.S = S, rk.NC = NC, rk.T = W * S - 2 * K;
         return rk;
     }
     if (h->force_tile == 0 || h->force_slab == 0) return rk;
@@ -524,7 +526,7 @@ hipError_t launch_auto(golhip_t h, int K, const uint32_t *in, uint32_t *out,
         q.nbands = q.nbands0 + (p.r1e - p.r1b + T - 1) / T;
         q.nchunks = (int32_t)((h->wd + golhip::kTileChunkWords - 1) / golhip::kTileChunkWords);
         return rk.kind == 2 ? golhip::launch_stencil_tile(K, T, in, out, q, slots, s)
-                            : golhip::launch_stencil_slab(K, rk.W, rk.S, in, out, q, slots, s);
+                            : golhip::launch_stencil_slab(K, rk.W, rk.S, rk.NC, in, out, q, slots, s);
     }
     const int S = pick_split(h, rows_total, K);
     if (S > 1) {
@@ -1563,7 +1565,7 @@ int golhip_launch_kind(golhip_t h, int k, int *kind, int *param) {
     const int64_t rows = h->shards[0].rows;
     if (const RegKernel rk = pick_reg_kernel(h, rows, k); rk.kind) {
         *kind = rk.kind;
-        *param = rk.kind == 2 ? rk.T : rk.W * 100 + rk.S;
+        *param = rk.kind == 2 ? rk.T : (rk.NC != 4 ? rk.NC * 10000 : 0) + rk.W * 100 + rk.S;
     } else if (const int S = pick_split(h, rows, k); S > 1) {
         *kind = 1;
         *param = S;

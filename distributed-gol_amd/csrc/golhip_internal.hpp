@@ -121,10 +121,11 @@ hipError_t launch_stencil_tile(int K, int T, const uint32_t *in_row0, uint32_t *
 bool stencil_tile_supported(int K, int T);
 // Register slab (stencil_tile.hip): a workgroup of W waves, S rows each, edge rows swapped through
 // LDS every generation; T = W*S - 2K output rows per workgroup.
-hipError_t launch_stencil_slab(int K, int W, int S, const uint32_t *in_row0, uint32_t *out_row0,
+// NC: independent row chains per wave (segments advanced op-major).
+hipError_t launch_stencil_slab(int K, int W, int S, int NC, const uint32_t *in_row0, uint32_t *out_row0,
                                const StencilParams &p, unsigned long long *count_slots,
                                hipStream_t s);
-bool stencil_slab_supported(int K, int W, int S);
+bool stencil_slab_supported(int K, int W, int S, int NC = 4);
 hipError_t warm_stencil_tile(hipStream_t s);
 constexpr int kTileChunkWords = 62;
 // Words per column chunk of the level-split kernel (half-word halo for K <= 16).

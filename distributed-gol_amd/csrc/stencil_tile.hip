@@ -28,6 +28,7 @@ namespace {
 
 // Independent row chains per wave (segments advanced op-major).
 constexpr int kTileChains = 4;
+constexpr int kXcds = 8;  // MI355X: 8 XCDs, workgroups dealt round-robin
 
 // Drifting 3-cell sums (row_sum3_drift) of N rows, op-major: each op for every row before the
 // next op, so the N dependency chains interleave.  Rows with use(i) false are skipped.
@@ -88,69 +89,85 @@ __device__ __forceinline__ void life_om(const uint32_t (&as)[N], const uint32_t 
 // Segment geometry of one generation step i: NS segments over rows [LO, LO + N), segment sg =
 // [first(sg), first(sg + 1)); active: it has a row at step I; fresh: that row's successor needs
 // new sums (not the segment's last row before a next segment, whose first m is saved).
-template <int LO, int N, int NS, int I>
+// Segment geometry of one generation step I: NS segments over rows [LO, LO + N), segment sg =
+// [first(sg), first(sg + 1)), walked top-down -- except segment 0 when REV0, walked bottom-up, so
+// that the row above the range (an LDS hand-off in gol_slab) is needed only at its LAST step.
+// fresh_row: the row whose sums step I takes fresh, -1 when it takes the saved sums of the next
+// segment's first row (a top-down segment's last row: that row may be overwritten already).
+template <int LO, int N, int NS, bool REV0, int I>
 struct TileStep {
     static constexpr int first(int sg) { return LO + (N * sg) / NS; }
+    static constexpr bool rev(int sg) { return REV0 && sg == 0; }
+    static constexpr bool active(int sg) { return first(sg) + I < first(sg + 1); }
+    static constexpr int row(int sg) { return rev(sg) ? first(sg + 1) - 1 - I : first(sg) + I; }
+    static constexpr int fresh_row(int sg) {
+        return !active(sg)                                          ? -1
+               : rev(sg)                                            ? row(sg) - 1
+               : (row(sg) + 1 == first(sg + 1) && sg + 1 < NS) ? -1
+                                                                    : row(sg) + 1;
+    }
     struct Active {
-        constexpr bool operator()(int sg) const { return first(sg) + I < first(sg + 1); }
+        constexpr bool operator()(int sg) const { return active(sg); }
     };
     struct Fresh {
-        constexpr bool operator()(int sg) const {
-            return first(sg) + I < first(sg + 1) && (first(sg) + I + 1 < first(sg + 1) || sg + 1 == NS);
-        }
+        constexpr bool operator()(int sg) const { return fresh_row(sg) >= 0; }
     };
 };
 
 // One generation over rows [LO, LO + N) of c (compile time) from the previous generation's rows
 // [LO - 1, LO + N].  The rows are cut into NS segments that advance together, op-major (one op
-// of every segment, then the next op): NS independent dependency chains per wave.  Each segment
-// walks its rows top to bottom holding the sums of the rows above (a), at (m) and below (b) the
-// row; row r is overwritten (WRITE) once its successor's sums are taken, so the update is in
-// place.  Every sum comes from the previous generation: a segment's first a/m are taken before
-// any row is written, and its last row's b is the next segment's first m (saved then).
+// of every segment, then the next op): NS independent dependency chains per wave.  A segment
+// walks its rows holding the sums of the rows on both sides of the current row: (o) the one
+// already passed and (m) the row itself; each step takes the sums of the next row, writes the
+// row's new cells (WRITE) and rotates o <- m <- new.  The rule is symmetric in the rows above
+// and below, so top-down and bottom-up segments run the same code.  Every sum comes from the
+// previous generation: the first o/m of every segment are taken before any row is written, and a
+// top-down segment's last row takes the next segment's first m (saved then).
 // emit(integral_constant<r>, next, centre) sees every new row and the centre cells it replaces
 // (same drifted frame: the last generation's flips are next ^ centre).
-template <int LO, int N, bool WRITE, int R, class F>
+template <int LO, int N, bool WRITE, int NC = kTileChains, bool REV0 = false, int R, class F>
 __device__ __forceinline__ void gen_rows(uint32_t (&c)[R], F &&emit) {
-    constexpr int NS = N < kTileChains ? N : kTileChains;
-    using TS0 = TileStep<LO, N, NS, 0>;
+    constexpr int NS = N < NC ? N : NC;
+    using TS0 = TileStep<LO, N, NS, REV0, 0>;
     constexpr int L = (N + NS - 1) / NS;
-    uint32_t as[NS], acy[NS], ms[NS], mcy[NS], mc[NS], ss[NS], scy[NS];
+    uint32_t os[NS], ocy[NS], ms[NS], mcy[NS], mc[NS], ss[NS], scy[NS];
     {
         uint32_t x[2 * NS], s2[2 * NS], cy2[2 * NS], c2[2 * NS];
 #pragma unroll
         for (int sg = 0; sg < NS; ++sg) {
-            x[2 * sg] = c[TS0::first(sg) - 1];
-            x[2 * sg + 1] = c[TS0::first(sg)];
+            // top-down: o = the row above the first, m = the first; bottom-up: o = the row below
+            // the last (the next segment's first row, still unwritten here), m = the last
+            x[2 * sg] = TS0::rev(sg) ? c[TS0::first(sg + 1)] : c[TS0::first(sg) - 1];
+            x[2 * sg + 1] = TS0::rev(sg) ? c[TS0::first(sg + 1) - 1] : c[TS0::first(sg)];
         }
         sums_om<2 * NS>(x, s2, cy2, c2);
 #pragma unroll
         for (int sg = 0; sg < NS; ++sg) {
-            as[sg] = s2[2 * sg], acy[sg] = cy2[2 * sg];
+            os[sg] = s2[2 * sg], ocy[sg] = cy2[2 * sg];
             ms[sg] = ss[sg] = s2[2 * sg + 1], mcy[sg] = scy[sg] = cy2[2 * sg + 1];
             mc[sg] = c2[2 * sg + 1];
         }
     }
     static_for(std::make_integer_sequence<int, L>{}, [&](auto ic) {
         constexpr int i = decltype(ic)::value;
-        using TS = TileStep<LO, N, NS, i>;
+        using TS = TileStep<LO, N, NS, REV0, i>;
         constexpr typename TS::Active active{};
         constexpr typename TS::Fresh fresh{};
         uint32_t x[NS], bs[NS], bcy[NS], bc[NS], nx[NS];
 #pragma unroll
-        for (int sg = 0; sg < NS; ++sg) x[sg] = fresh(sg) ? c[TS::first(sg) + i + 1] : 0u;
+        for (int sg = 0; sg < NS; ++sg) x[sg] = fresh(sg) ? c[TS::fresh_row(sg)] : 0u;
         sums_om<NS>(x, bs, bcy, bc, fresh);
 #pragma unroll
         for (int sg = 0; sg < NS; ++sg)
             if (active(sg) && !fresh(sg)) bs[sg] = ss[sg + 1], bcy[sg] = scy[sg + 1], bc[sg] = 0u;
-        life_om<NS>(as, acy, ms, mcy, mc, bs, bcy, nx, active);
+        life_om<NS>(os, ocy, ms, mcy, mc, bs, bcy, nx, active);
         static_for(std::make_integer_sequence<int, NS>{}, [&](auto sgc) {
             constexpr int sg = decltype(sgc)::value;
-            if constexpr (active(sg)) {
-                constexpr int r = TS::first(sg) + i;
+            if constexpr (TS::active(sg)) {
+                constexpr int r = TS::row(sg);
                 emit(std::integral_constant<int, r>{}, nx[sg], mc[sg]);
                 if constexpr (WRITE) c[r] = nx[sg];
-                as[sg] = ms[sg], acy[sg] = mcy[sg];
+                os[sg] = ms[sg], ocy[sg] = mcy[sg];
                 ms[sg] = bs[sg], mcy[sg] = bcy[sg], mc[sg] = bc[sg];
             }
         });
@@ -268,7 +285,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) voi
 // by generation parity: one barrier per generation) and update their S rows.  The trapezoid is
 // paid once per slab (2K rows of W*S) instead of once per wave, with S-row waves: more waves per
 // SIMD at the same work.  Output: the T = W*S - 2K middle rows.
-template <int K, int W, int S, bool COUNT, bool LD>
+template <int K, int W, int S, bool COUNT, bool LD, int NC = kTileChains>
 __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ in,
                                                    uint32_t *__restrict__ out, StencilParams p,
                                                    unsigned long long *__restrict__ slots) {
@@ -280,10 +297,17 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
     __shared__ uint32_t cnt_lds[COUNT ? K : 1][64];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int64_t group = blockIdx.x;
+    // XCD-aware order: the dispatcher deals workgroups round-robin over the 8 XCDs (each with its
+    // own L2), so workgroup b runs on XCD b % 8.  Give XCD x a contiguous range of slabs (all
+    // column chunks of consecutive bands): the halo rows and halo lanes a slab reads were written
+    // by its neighbours in the previous launch on the SAME XCD, i.e. they hit that L2, except at
+    // the 8 range seams.
+    const int64_t ngroups = p.nbands * (int64_t)p.nchunks;
+    const int64_t per_xcd = (ngroups + kXcds - 1) / kXcds;
+    const int64_t group = (int64_t)(blockIdx.x % kXcds) * per_xcd + blockIdx.x / kXcds;
+    if (group >= ngroups) return;  // whole workgroup (grid padded to whole XCD rounds)
     const int64_t chunk = group % p.nchunks;
     const int64_t bandi = group / p.nchunks;
-    if (bandi >= p.nbands) return;  // whole workgroup
     int ya, yb;
     band_rows(p, bandi, ya, yb);  // yb - ya <= T (the host sets p.band = T)
     const int nrows = yb - ya;
@@ -322,7 +346,9 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
     auto pass = [&](auto last_c, auto full_c, int gen) {
         constexpr bool LAST = decltype(last_c)::value, FULL = decltype(full_c)::value;
         uint32_t cnt = 0;
-        gen_rows<1, S, !LAST>(c, [&](auto rc, uint32_t nx, uint32_t centre) {
+        // (segment 0 bottom-up, REV0 -- the hand-off row above needed only at its last step --
+        // measured 3-7 % slower: profiles/r02/small_boards.txt)
+        gen_rows<1, S, !LAST, NC>(c, [&](auto rc, uint32_t nx, uint32_t centre) {
             constexpr int r = decltype(rc)::value;
             const int o = o0 + r - 1;
             const bool mine = FULL || (o >= 0 && o < nrows);  // wave-uniform
@@ -382,44 +408,47 @@ hipError_t launch_tile_kt(const uint32_t *in, uint32_t *out, const StencilParams
     return hipGetLastError();
 }
 
-template <int K, int W, int S>
+template <int K, int W, int S, int NC>
 hipError_t launch_slab_kws(const uint32_t *in, uint32_t *out, const StencilParams &p,
                            unsigned long long *slots, hipStream_t s) {
-    const unsigned blocks = (unsigned)std::max<int64_t>(1, p.nbands * (int64_t)p.nchunks);
+    const int64_t ngroups = p.nbands * (int64_t)p.nchunks;
+    const unsigned blocks = (unsigned)std::max<int64_t>(1, (ngroups + kXcds - 1) / kXcds * kXcds);
     const dim3 block(64 * W);
     if (p.diff) {
         if (slots)
-            hipLaunchKernelGGL((gol_slab<K, W, S, true, true>), dim3(blocks), block, 0, s, in, out, p, slots);
+            hipLaunchKernelGGL((gol_slab<K, W, S, true, true, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
         else
-            hipLaunchKernelGGL((gol_slab<K, W, S, false, true>), dim3(blocks), block, 0, s, in, out, p, slots);
+            hipLaunchKernelGGL((gol_slab<K, W, S, false, true, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
     } else if (slots) {
-        hipLaunchKernelGGL((gol_slab<K, W, S, true, false>), dim3(blocks), block, 0, s, in, out, p, slots);
+        hipLaunchKernelGGL((gol_slab<K, W, S, true, false, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
     } else {
-        hipLaunchKernelGGL((gol_slab<K, W, S, false, false>), dim3(blocks), block, 0, s, in, out, p, slots);
+        hipLaunchKernelGGL((gol_slab<K, W, S, false, false, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
     }
     return hipGetLastError();
 }
 
 }  // namespace
 
+// (K, waves, rows per wave, interleaved row chains)
 #define GOLHIP_SLAB_CONFIGS(X) \
-    X(8, 8, 4) X(8, 8, 8) X(8, 16, 4) X(8, 16, 8) X(12, 8, 8) X(12, 16, 4) X(12, 16, 8) \
-    X(16, 8, 8) X(16, 8, 10) X(16, 8, 11) X(16, 8, 12) X(16, 8, 13) X(16, 8, 14) X(16, 8, 16) \
-    X(16, 8, 20) X(16, 8, 24) X(16, 16, 4) X(16, 16, 6) X(16, 16, 8) X(16, 16, 16) X(16, 4, 16) \
-    X(16, 4, 24)
+    X(8, 8, 4, 4) X(8, 8, 8, 4) X(8, 16, 4, 4) X(8, 16, 8, 4) X(12, 8, 8, 4) X(12, 16, 4, 4) \
+    X(12, 16, 8, 4) X(16, 8, 8, 4) X(16, 8, 10, 4) X(16, 8, 11, 4) X(16, 8, 12, 4) X(16, 8, 13, 4) \
+    X(16, 8, 14, 4) X(16, 8, 16, 4) X(16, 8, 20, 4) X(16, 8, 24, 4) X(16, 16, 4, 4) X(16, 16, 6, 4) \
+    X(16, 16, 8, 4) X(16, 16, 16, 4) X(16, 4, 16, 4) X(16, 4, 24, 4) X(16, 8, 12, 2) X(16, 8, 12, 3)
 
-bool stencil_slab_supported(int K, int W, int S) {
-#define GOLHIP_X(KK, WW, SS) \
-    if (K == KK && W == WW && S == SS) return true;
+bool stencil_slab_supported(int K, int W, int S, int NC) {
+#define GOLHIP_X(KK, WW, SS, NN) \
+    if (K == KK && W == WW && S == SS && NC == NN) return true;
     GOLHIP_SLAB_CONFIGS(GOLHIP_X)
 #undef GOLHIP_X
     return false;
 }
 
-hipError_t launch_stencil_slab(int K, int W, int S, const uint32_t *in_row0, uint32_t *out_row0,
+hipError_t launch_stencil_slab(int K, int W, int S, int NC, const uint32_t *in_row0, uint32_t *out_row0,
                                const StencilParams &p, unsigned long long *slots, hipStream_t s) {
-#define GOLHIP_X(KK, WW, SS) \
-    if (K == KK && W == WW && S == SS) return launch_slab_kws<KK, WW, SS>(in_row0, out_row0, p, slots, s);
+#define GOLHIP_X(KK, WW, SS, NN) \
+    if (K == KK && W == WW && S == SS && NC == NN) \
+        return launch_slab_kws<KK, WW, SS, NN>(in_row0, out_row0, p, slots, s);
     GOLHIP_SLAB_CONFIGS(GOLHIP_X)
 #undef GOLHIP_X
     return hipErrorInvalidValue;

@@ -430,22 +430,24 @@ def test_register_tile_tracked_flips(golhip, oracle, monkeypatch, k):
 SLAB_CONFIGS = [(8, 8, 4), (8, 8, 8), (8, 16, 4), (8, 16, 8), (12, 8, 8), (12, 16, 4), (12, 16, 8),
                 (16, 8, 8), (16, 8, 10), (16, 8, 11), (16, 8, 12), (16, 8, 13), (16, 8, 14), (16, 8, 16),
                 (16, 8, 20), (16, 8, 24), (16, 16, 4), (16, 16, 6), (16, 16, 8), (16, 16, 16), (16, 4, 16),
-                (16, 4, 24)]
+                (16, 4, 24), (16, 8, 12, 2), (16, 8, 12, 3)]
 
 
-@pytest.mark.parametrize("k,waves,rows", SLAB_CONFIGS)
-def test_register_slab_kernel(golhip, oracle, monkeypatch, k, waves, rows):
+@pytest.mark.parametrize("cfg", SLAB_CONFIGS)
+def test_register_slab_kernel(golhip, oracle, monkeypatch, cfg):
     """The register-slab stencil (gol_slab: W waves x S rows of a 62-word chunk in VGPRs, edge
     rows swapped through LDS every generation) forced at every compiled (K, W, S): wrap, boards
     shorter than a slab, ragged widths, short last slabs, per-turn counts."""
-    monkeypatch.setenv("GOLHIP_SLAB", str(waves * 100 + rows))
+    k, waves, rows = cfg[:3]
+    code = (cfg[3] * 10000 if len(cfg) > 3 else 0) + waves * 100 + rows
+    monkeypatch.setenv("GOLHIP_SLAB", str(code))
     for (h, w) in [(77, 640), (16, 16), (5, 96), (300, 4160), (129, 200), (40, 8192), (250, 1984)]:
         rng = np.random.default_rng(h * 7 + w + k + waves + rows)
         board = ((rng.random((h, w)) < 0.4) * 255).astype(np.uint8)
         turns = 3 * k + 1
         exp, exp_counts = oracle.packed_run(board, turns)
         with golhip.Engine(w, h, k=k) as e:
-            assert e.launch_kind(k) == ("slab", waves * 100 + rows)
+            assert e.launch_kind(k) == ("slab", code)
         out, counts, _, _ = run_engine(golhip, board, turns, k=k, counts=True)
         assert np.array_equal(out, exp), (k, waves, rows, h, w)
         assert np.array_equal(counts.astype(np.int64), exp_counts), (k, waves, rows, h, w)
