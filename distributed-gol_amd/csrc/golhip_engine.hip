@@ -488,8 +488,9 @@ RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K) {
     // -- 1.33 us per turn with counts vs 1.62 for the level split, 1.21 vs 1.35 at 4096^2, 2.45
     // vs 2.87 at 8192^2), on boards where the streaming kernel has fewer than four minimal-band
     // waves per SIMD
-    int W = 8, S = K == 16 ? 12 : 8;
-    if (!golhip::stencil_slab_supported(K, W, S)) return rk;
+    // (2 row chains per wave at 8 x 12: 1 % over 4, fewer segment-start sums)
+    const int W = 8, S = K == 16 ? 12 : 8, NC = K == 16 ? 2 : 4;
+    if (!golhip::stencil_slab_supported(K, W, S, NC)) return rk;
     const int64_t per = golhip::chunk_words(K, h->variant);
     const int64_t nchunks = (h->wd + per - 1) / per;
     const int64_t minband = std::max(K, 8);
@@ -501,7 +502,7 @@ RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K) {
                      : 256;
     }
     if (waves1 > 16 * (int64_t)h->cus) return rk;
-    rk.kind = 3, rk.W = W, rk.S = S, rk.T = W * S - 2 * K;
+    rk.kind = 3, rk.W = W, rk.S = S, rk.NC = NC, rk.T = W * S - 2 * K;
     return rk;
 }
 
@@ -874,8 +875,8 @@ int create_common(golhip_t h) {
 constexpr int kGraphGens = 128;      // generations per graph replay (<= count_window)
 // Long runs replay larger graphs: each replay of a counting graph ends in a count finalize and a
 // copy of its counts (~17 us together on a 5120^2 board, profiles/r02/small_board_timeline.txt),
-// paid per 1024 generations instead of per 128.
-constexpr int kGraphGensBig = 1024;
+// paid per 4096 generations instead of per 128 (bounded by the count window).
+constexpr int kGraphGensBig = 4096;
 
 // Graphs pay off when a launch is short (launch-bound): < ~100 us of stencil work.
 bool small_board(double cells, int K) { return cells * K <= 8e9; }

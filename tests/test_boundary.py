@@ -102,9 +102,9 @@ def test_launch_plan_small_boards_replay_graphs(golhip):
 
 
 def test_launch_plan_long_runs_replay_large_graphs(golhip):
-    """Long small-board runs replay 1024-generation graphs (one count finalize + copy per replay),
+    """Long small-board runs replay 4096-generation graphs (one count finalize + copy per replay),
     then 128-generation graphs, then single launches."""
     plan = golhip.launch_plan(5120, 5120, 16, 10000)
     graphs = [-d for d in plan if d < 0]
-    assert graphs[:9] == [1024] * 9 and set(graphs[9:]) <= {128}
+    assert graphs[:2] == [4096] * 2 and set(graphs[2:]) <= {128}
     assert sum(graphs) + sum(d for d in plan if d > 0) == 10000

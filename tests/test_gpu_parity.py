@@ -476,7 +476,7 @@ def test_small_board_picks_register_slab(golhip, oracle):
     depth choice); results unchanged, counts every turn."""
     words = oracle.init_random(5120, 512, seed=2)
     with golhip.Engine(5120, 512, k=16) as e:
-        assert e.launch_kind(16) == ("slab", 812)
+        assert e.launch_kind(16) == ("slab", 20812)
         assert e.launch_kind(8) == ("slab", 808)
         e.load_words(words)
         counts = e.step(200, counts=True)
