@@ -278,10 +278,13 @@ def main():
                 "mix": "12 per 32-cell word per generation: 9 v_bitop3 (2 cyc) + 2 v_alignbit "
                        "+ 1 DPP move (4 cyc): mix_peak = 24/30 of peak",
                 "mix_peak": round(VALU_PEAK_T * 24 / VALU_CYCLES_PER_WORD_GEN, 4)}
-        if issued and uniform:
-            roof["issued_pmc"] = round(issued / (avg_launch_ms * 1e-3) / 1e12, 4)
-            roof["issued_frac"] = round(issued / (avg_launch_ms * 1e-3) / 1e12 / VALU_PEAK_T, 4)
+        if issued:
+            # PMC SQ_INSTS_VALU of one gol_stencil<dominant_k> launch (profiles/pmc_traffic.json);
+            # the issue RATE needs every timed launch to be that kernel
             roof["issued_per_launch_pmc"] = issued
+            if uniform:
+                roof["issued_pmc"] = round(issued / (avg_launch_ms * 1e-3) / 1e12, 4)
+                roof["issued_frac"] = round(issued / (avg_launch_ms * 1e-3) / 1e12 / VALU_PEAK_T, 4)
         if pmc_entry.get("clock_ghz"):
             roof["clock_ghz_pmc"] = pmc_entry["clock_ghz"]
     roof.update({"kernel": kernel_name, "avg_launch_us": round(avg_launch_ms * 1e3, 2),
