@@ -30,7 +30,16 @@ Prints ONE JSON line on rank 0 (keys per the driver contract), plus:
   k_sweep      : GCUPS per temporal-blocking depth k (N == 1 only);
   hbm_roofline_k1: the k = 1 kernel (gol_step1, no temporal reuse) against the HBM peak;
   strong_262144: configs[3] -- the 262144^2 board (seed 4) split over the N ranks, GCUPS and
-                 GCUPS per GPU (strong scaling of one fixed board; --no-strong skips it).
+                 GCUPS per GPU (strong scaling of one fixed board; --no-strong skips it);
+  configs      : configs[0], [1], [4] on the GPU (512^2 PGM x 100, 5120^2 x 10 000 and 4096^2 x
+                 1e6 turns, every count), each checked against the reference fixture / goldens;
+  cold_start   : the same warmup + timed turns run first, on the chip as the process found it.
+
+Timing order: cold-start pass (warmup + steps, reported as cold_start) -> --preheat-ms of untimed
+K-deep launches -> the board is re-initialised from the seed -> warmup -> the timed steps (value).
+The MI355X's clock ramps over the first tens of ms of load: a 20-turn region right after an idle
+start runs ~10 % slower than the same turns on a loaded chip (profiles/r02/r02r_preheat.txt), so
+value is the loaded-clock rate and cold_start keeps the idle-start figure beside it.
 """
 from __future__ import annotations
 
@@ -85,8 +94,15 @@ def parse():
     ap.add_argument("--no-strong", action="store_true",
                     help="skip the configs[3] leg (262144^2 board split over the N ranks)")
     ap.add_argument("--no-flips", action="store_true", help="skip the per-turn CellFlipped leg")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the configs[0]/[1]/[4] leg (512^2 PGM, 5120^2 and 4096^2 with every count)")
     ap.add_argument("--strong-size", type=int, default=262144)
     ap.add_argument("--strong-steps", type=int, default=160)
+    ap.add_argument("--preheat-ms", type=float, default=200.0,
+                    help="after a cold-start pass of the same turns (reported as cold_start), "
+                         "untimed K-deep launches for this long, then the board is re-initialised "
+                         "from the seed and warmup + timed turns run on a chip at its loaded clock "
+                         "(0 = off: the timed turns are the cold start)")
     return ap.parse_args()
 
 
@@ -147,6 +163,17 @@ def cpu_baseline(size: int, turns: int, threads_per_server: int) -> dict:
     dt512 = time.perf_counter() - t0
     exact = oracle.pgm_bytes(out512) == (ref / "check" / "images" / "512x512x100.pgm").read_bytes()
 
+    # configs[1] prefix: 5120^2 seed 2, the first 20 of its 10 000 turns, every count checked
+    # against the golden CSV (the oracle's own per-turn counts)
+    gold = json.loads((GOLDEN / "synthetic_golden.json").read_text())
+    lines = (GOLDEN / gold["cfg2"]["counts_csv"]).read_text().split()[1:21]
+    b2 = oracle.unpack(oracle.init_random(5120, 5120, seed=2), 5120)
+    t0 = time.perf_counter()
+    _, c2 = oracle.ref_run(b2, 20, threads=threads_per_server, servers=4, fanout_copy=True)
+    dt2 = time.perf_counter() - t0
+    ok2 = [int(x) for x in c2] == [int(ln.split(",")[1]) for ln in lines]
+    del b2
+
     board = oracle.unpack(oracle.init_random(size, size, seed=3), size)
     t0 = time.perf_counter()
     oracle.ref_run(board, turns, threads=threads_per_server, servers=4, fanout_copy=True)
@@ -168,6 +195,10 @@ def cpu_baseline(size: int, turns: int, threads_per_server: int) -> dict:
                    f"transport not timed; {dt:.1f} s"),
         "cfg1_512x100": {"s": round(dt512, 4), "gcups": round(512 * 512 * 100 / dt512 / 1e9, 4),
                          "bit_exact_vs_reference_fixture": bool(exact)},
+        "cfg2_5120_first20": {"s": round(dt2, 4), "gcups": round(5120 * 5120 * 20 / dt2 / 1e9, 4),
+                              "us_per_turn": round(dt2 / 20 * 1e6, 1),
+                              "counts_match_golden": bool(ok2),
+                              "sample": "first 20 of configs[1]'s 10 000 turns (labelled prefix)"},
     }
 
 
@@ -192,6 +223,102 @@ def golden_count_cfg4(turn: int) -> int | None:
         if int(t) == turn:
             return int(c)
     return None
+
+
+def read_pgm_body(path: Path) -> tuple[int, int, bytes]:
+    """P5 header "P5\\n<w> <h>\\n255\\n" (gol/io.go:52-59) -> (width, height, pixel bytes)."""
+    raw = path.read_bytes()
+    fields, pos = [], 0
+    while len(fields) < 4:
+        while raw[pos:pos + 1].isspace():
+            pos += 1
+        end = pos
+        while not raw[end:end + 1].isspace():
+            end += 1
+        fields.append(raw[pos:end])
+        pos = end
+    pos += 1  # the single whitespace byte after maxval
+    w, h = int(fields[1]), int(fields[2])
+    return w, h, raw[pos:pos + w * h]
+
+
+def configs_leg() -> dict:
+    """BASELINE.json configs[0], [1] and [4] on this GPU through the production path (automatic
+    kernel choice, default planner), each checked against the reference fixture / oracle goldens:
+      cfg1: images/512x512.pgm, 100 turns with every count -> check/images/512x512x100.pgm
+            byte-exact and all 100 counts of check/alive/512x512.csv;
+      cfg2: 5120^2 random seed 2, 10 000 turns with every count (tests/golden cfg2 CSV);
+      cfg5: 4096^2 glider gun + R-pentomino, 1e6 turns with every count (tests/golden cfg5 npz).
+    Wall time of the golhip_step call(s) incl. the per-turn count copy to the host."""
+    import numpy as np
+
+    gold = json.loads((GOLDEN / "synthetic_golden.json").read_text())
+    ref = GOLDEN / "reference"
+    res = {}
+    # configs[0]
+    w, h, px = read_pgm_body(ref / "images" / "512x512.pgm")
+    board = np.frombuffer(px, dtype=np.uint8).reshape(h, w)
+    _, _, want = read_pgm_body(ref / "check" / "images" / "512x512x100.pgm")
+    csv = [ln.split(",") for ln in (ref / "check" / "alive" / "512x512.csv").read_text().split()]
+    want_counts = {int(t): int(c) for t, c in (r for r in csv if r[0].strip().isdigit())}
+    with golhip.Engine(w, h, k=16) as e:
+        e.load(board)
+        e.step(100, counts=True)  # warm (graphs, code paths)
+        runs = []
+        for _ in range(5):
+            e.load(board)
+            e.sync()
+            t = time.perf_counter()
+            c = e.step(100, counts=True)
+            e.sync()
+            runs.append(time.perf_counter() - t)
+        out = e.store()
+    ok = (out.tobytes() == want and [int(x) for x in c] == [want_counts[t] for t in range(1, 101)])
+    dt = float(np.median(runs))
+    res["cfg1_512x100"] = {"us_per_turn": round(dt / 100 * 1e6, 3), "median_of": len(runs),
+                           "bit_exact_vs_reference_fixture": bool(ok)}
+    # configs[1]
+    lines = (GOLDEN / gold["cfg2"]["counts_csv"]).read_text().split()[1:]
+    exp2 = np.array([int(ln.split(",")[1]) for ln in lines], dtype=np.uint64)
+    with golhip.Engine(5120, 5120, k=16) as e:
+        kind = e.launch_kind(16)
+        runs, ok = [], True
+        for _ in range(5):
+            e.init_random(2)
+            e.sync()
+            t = time.perf_counter()
+            c = e.step(10000, counts=True)
+            runs.append(time.perf_counter() - t)
+            ok = ok and bool(np.array_equal(c.astype(np.uint64), exp2))
+    runs_sorted = sorted(runs[1:])  # the first run captures the count graphs
+    dt = runs_sorted[len(runs_sorted) // 2]
+    res["cfg2_5120x10000"] = {"us_per_turn": round(dt / 10000 * 1e6, 3),
+                              "best_us_per_turn": round(runs_sorted[0] / 10000 * 1e6, 3),
+                              "runs_s": [round(r, 4) for r in runs],
+                              "gcups": round(5120 * 5120 * 10000 / dt / 1e9, 1),
+                              "counts_match_all_10000": ok, "kernel": f"{kind[0]}{kind[1] or ''}"}
+    # configs[4]
+    b = np.zeros((4096, 4096), dtype=np.uint8)
+    golhip.place(b, golhip.parse_rle((GOLDEN / "gosper_gun.rle").read_text()), 64, 64)
+    golhip.place(b, golhip.parse_rle((GOLDEN / "r_pentomino.rle").read_text()), 2048, 2048)
+    deltas = np.load(GOLDEN / gold["cfg5"]["counts_1e6_npz"])["deltas"]
+    exp5 = (int((b == 255).sum()) + np.cumsum(deltas.astype(np.int64))).astype(np.uint64)
+    with golhip.Engine(4096, 4096, k=16) as e:
+        kind = e.launch_kind(16)
+        e.load(b)
+        e.step(4096, counts=True)  # capture the count graphs
+        e.load(b)
+        e.sync()
+        t = time.perf_counter()
+        c = e.step(1000000, counts=True)
+        dt = time.perf_counter() - t
+    res["cfg5_4096x1e6"] = {"us_per_turn": round(dt, 3), "gcups": round(4096 * 4096 * 1e6 / dt / 1e9, 1),
+                            "counts_match_all_1e6": bool(np.array_equal(c.astype(np.uint64), exp5)),
+                            "kernel": f"{kind[0]}{kind[1] or ''}"}
+    res["ok"] = bool(res["cfg1_512x100"]["bit_exact_vs_reference_fixture"]
+                     and res["cfg2_5120x10000"]["counts_match_all_10000"]
+                     and res["cfg5_4096x1e6"]["counts_match_all_1e6"])
+    return res
 
 
 def main():
@@ -219,6 +346,23 @@ def main():
         eng.set_band_rows(a.band_rows)
     eng.init_random(a.seed)
     local_rows = eng.info.rows
+    cold = None
+    if a.preheat_ms > 0:
+        # cold start: the same warmup + timed turns on a chip that was idle until now (its clock
+        # ramps up over the first tens of ms of load: profiles/r02/r02r_preheat.txt)
+        eng.step(a.warmup)
+        eng.sync()
+        dtc = timed_steps(eng, a.steps, world)
+        alive_c = eng.alive_count()  # collective
+        cold = {"value": round(width * height * a.steps / dtc / 1e9, 2),
+                "ms_per_step": round(dtc * 1e3 / a.steps, 4), "alive_after": int(alive_c)}
+        # pre-heat: untimed K-deep launches for preheat_ms, then the board starts from the seed
+        # again, so warmup + the timed turns below are exactly those of a fresh run
+        t0 = time.perf_counter()
+        while (time.perf_counter() - t0) * 1e3 < a.preheat_ms:
+            eng.step(4 * a.k)
+            eng.sync()
+        eng.init_random(a.seed)
     local_cells = local_rows * width
 
     eng.step(a.warmup)
@@ -302,6 +446,9 @@ def main():
         if exp is not None:
             parity = {"turn": a.warmup + a.steps, "alive": int(alive_timed), "golden": exp,
                       "ok": int(alive_timed) == exp}
+            if cold is not None:
+                parity["cold_start_ok"] = cold["alive_after"] == exp
+                parity["ok"] = parity["ok"] and parity["cold_start_ok"]
 
     sweep = None
     k1_launch_us = None
@@ -385,6 +532,10 @@ def main():
                                  "turns_per_call": T, "flips_per_turn": round(cells / (reps * T), 1),
                                  "us_per_turn_step1_then_flips": round(dt1 / 64 * 1e6, 2)}
 
+    small = None
+    if world == 1 and not a.no_configs:
+        small = configs_leg()
+
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
         cpu = cpu_baseline(a.cpu_size, a.cpu_turns, threads_per_server=4)
@@ -410,6 +561,10 @@ def main():
                 "width": width, "height": height, "k": a.k, "parallelism": f"rows{world}",
             },
             "parity": parity,
+            "preheat_ms": a.preheat_ms,
+            # the same warmup + timed turns measured first, on the chip as the process found it
+            # (idle clock): what a 20-turn run pays before the clock has ramped
+            "cold_start": cold,
             "roofline": roof,
             "hbm_roofline": hbm_roof,
             "cpu_baseline": cpu,
@@ -425,6 +580,7 @@ def main():
                 "frac": round(BYTES_PER_CELL_UPDATE * local_cells / k1_launch_us / 1e3 / HBM_PEAK_GBS, 4)},
             "strong_262144": strong,
             "flips_path": flips,
+            "configs": small,
             "alive_after_timed": int(alive_timed),
             "alive_after": int(checksum),
         }
@@ -432,7 +588,8 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     # a wrong board is not a result: the line above is printed for the record, then the run fails
-    bad = (parity and not parity["ok"]) or (strong and strong.get("parity") and not strong["parity"]["ok"])
+    bad = ((parity and not parity["ok"]) or (strong and strong.get("parity") and not strong["parity"]["ok"])
+           or (small and not small["ok"]))
     if bad:
         raise SystemExit("bench parity FAILED: alive count differs from the oracle's golden count")
 
