@@ -355,13 +355,17 @@ def main():
         dtc = timed_steps(eng, a.steps, world)
         alive_c = eng.alive_count()  # collective
         cold = {"value": round(width * height * a.steps / dtc / 1e9, 2),
+                "preheat_turns": None,
                 "ms_per_step": round(dtc * 1e3 / a.steps, 4), "alive_after": int(alive_c)}
-        # pre-heat: untimed K-deep launches for preheat_ms, then the board starts from the seed
-        # again, so warmup + the timed turns below are exactly those of a fresh run
-        t0 = time.perf_counter()
-        while (time.perf_counter() - t0) * 1e3 < a.preheat_ms:
-            eng.step(4 * a.k)
-            eng.sync()
+        # pre-heat: untimed K-deep launches for about preheat_ms, then the board starts from the
+        # seed again, so warmup + the timed turns below are exactly those of a fresh run.  The
+        # turn count comes from the cold pass's max-over-ranks time, so every rank runs the same
+        # number of steps (each step call exchanges halos over RCCL when N > 1)
+        pre_turns = max(a.k, int(a.preheat_ms / (dtc * 1e3 / a.steps)))
+        pre_turns = -(-pre_turns // a.k) * a.k
+        eng.step(pre_turns)
+        eng.sync()
+        cold["preheat_turns"] = pre_turns
         eng.init_random(a.seed)
     local_cells = local_rows * width
 
