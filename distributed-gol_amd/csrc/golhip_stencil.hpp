@@ -35,9 +35,18 @@
 namespace golhip {
 namespace {
 
+#ifdef GOLHIP_WEST_BPERM
+// Experiment (not the production build): the west word through the LDS crossbar (ds_bpermute)
+// instead of a DPP move, taking the cross-lane move off the VALU issue port.
+__device__ __forceinline__ uint32_t lane_from_west(uint32_t v) {  // lane i <- lane i-1
+    const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(((lane - 1) & 63) << 2, (int)v);
+}
+#else
 __device__ __forceinline__ uint32_t lane_from_west(uint32_t v) {  // lane i <- lane i-1
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138 /* wave_shr:1 */, 0xf, 0xf, false);
 }
+#endif
 __device__ __forceinline__ uint32_t lane_from_east(uint32_t v) {  // lane i <- lane i+1
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130 /* wave_shl:1 */, 0xf, 0xf, false);
 }

@@ -73,7 +73,8 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    p = Path(path) if path else LIB_PATH
+    # GOLHIP_LIB: an alternative build of the same library (A/B experiments); default in-tree
+    p = Path(path) if path else Path(os.environ.get("GOLHIP_LIB", str(LIB_PATH)))
     if not p.exists():
         raise GolHipError(ERR_NODEV, f"{p} not built (run __graft_entry__.build())")
     L = ctypes.CDLL(str(p))

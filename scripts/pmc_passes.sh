@@ -8,7 +8,7 @@ K=${1:-8}; shift || true
 OUT=gpurun_out/pmc_k${K}
 mkdir -p $OUT
 export TMPDIR=/tmp
-BENCH="python3 bench.py --no-cpu --no-sweep --no-strong --no-flips --steps $((2*K)) --warmup 0 --k $K $*"
+BENCH="python3 bench.py --no-cpu --no-sweep --no-strong --no-flips --no-configs --preheat-ms 0 --steps $((2*K)) --warmup 0 --k $K $*"
 i=0
 for CTRS in "FETCH_SIZE" "WRITE_SIZE" \
             "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU" \
