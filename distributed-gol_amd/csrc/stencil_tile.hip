@@ -339,12 +339,30 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
         lds_barrier();
         c[0] = w > 0 ? ex[par][w - 1][1][lane] : 0u;
         c[S + 1] = w < W - 1 ? ex[par][w + 1][0][lane] : 0u;
+        if constexpr (COUNT && 2 * S <= K) {
+            // Generation g - 2 (0-based) is complete in LDS after this barrier.  With 2S <= K,
+            // waves 0 and W - 1 hold only halo rows, dead from generation S on (g_end below),
+            // i.e. for at least half the launch: they take turns summing and flushing one
+            // complete generation per exchange while the other waves compute, instead of every
+            // generation's flush queueing at the end of the launch.  (Measured: with S = 12 of
+            // K = 16 the same scheme is slower than the end flush, and so is letting the two
+            // waves flush in batches once idle: profiles/r02/r02aa_slab_flush.txt.)
+            if (g >= 2 && w == ((g & 1) ? W - 1 : 0)) {
+                uint32_t acc[1] = {cnt_lds[g - 2][lane]};
+                flush_counts<1>(acc, g - 2, lane, group, slots);
+            }
+        }
     };
     // FULL: every row of this wave is an output row of the band (interior waves): the counts need
     // no per-row mask (one v_bcnt per row instead of a select and a v_bcnt)
     const bool full = o0 >= 0 && o0 + S <= nrows;
-    auto pass = [&](auto last_c, auto full_c, int gen) {
+    // HALO: no row of this wave is an output row of the band (the slab's K-row halos, or rows past
+    // a short last band): it never counts and never stores, so it skips the last generation, and
+    // any generation at which all its rows are already outside the trapezoid [g, W*S - g)
+    const bool halo = o0 + S <= 0 || o0 >= nrows;
+    auto pass = [&](auto last_c, auto full_c, auto cnt_c, int gen) {
         constexpr bool LAST = decltype(last_c)::value, FULL = decltype(full_c)::value;
+        constexpr bool CNT = COUNT && decltype(cnt_c)::value;
         uint32_t cnt = 0;
         // (segment 0 bottom-up, REV0 -- the hand-off row above needed only at its last step --
         // measured 3-7 % slower: profiles/r02/small_boards.txt)
@@ -352,7 +370,7 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
             constexpr int r = decltype(rc)::value;
             const int o = o0 + r - 1;
             const bool mine = FULL || (o >= 0 && o < nrows);  // wave-uniform
-            if (COUNT) cnt += __builtin_popcount(mine ? nx : 0u);
+            if (CNT) cnt += __builtin_popcount(mine ? nx : 0u);
             if constexpr (LAST) {
                 const int rowoff = mine ? o * rowbytes : kOutOfRange;
                 Words<1> v;
@@ -365,27 +383,65 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
                 }
             }
         });
-        if constexpr (COUNT)
+        if constexpr (CNT)
             if (count_lane) __hip_atomic_fetch_add(&cnt_lds[gen][lane], cnt, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_WORKGROUP);
     };
     using No = std::false_type;
     using Yes = std::true_type;
+    // One generation loop per wave kind, each with a single pass body (a branch between pass
+    // variants inside the loop makes the allocator reconcile c[] with v_movs every generation).
+    // Slab rows [w*S, w*S + S) of this wave; generation g is valid on [g, W*S - g), so from
+    // generation g_end = min(w*S + S, W*S - w*S) on all of a wave's rows are outside it.
+    if constexpr (!COUNT) {
+        // without counts every wave runs every generation: measured faster than skipping the
+        // halo waves' dead generations (0.815 vs 0.847 us/turn at 5120^2, profiles/r02/r02z_slab_ab.txt)
 #pragma clang loop unroll(disable)
-    for (int g = 1; g < K; ++g) {
-        exchange(g);
-        if (COUNT && full)
-            pass(No{}, Yes{}, g - 1);
-        else
-            pass(No{}, No{}, g - 1);
+        for (int g = 1; g < K; ++g) {
+            exchange(g);
+            pass(No{}, No{}, No{}, g - 1);
+        }
+        exchange(K);
+        pass(Yes{}, No{}, No{}, K - 1);
+    } else if (halo) {
+        const int g_end = std::min(std::min(w * S + S, W * S - w * S), K);
+        int g = 1;
+#pragma clang loop unroll(disable)
+        for (; g < g_end; ++g) {
+            exchange(g);
+            pass(No{}, No{}, No{}, g - 1);
+        }
+#pragma clang loop unroll(disable)
+        for (; g <= K; ++g) exchange(g);  // its edge rows are garbage: nothing reads them as valid
+    } else {
+        if (COUNT && full) {
+#pragma clang loop unroll(disable)
+            for (int g = 1; g < K; ++g) {
+                exchange(g);
+                pass(No{}, Yes{}, Yes{}, g - 1);
+            }
+        } else {
+#pragma clang loop unroll(disable)
+            for (int g = 1; g < K; ++g) {
+                exchange(g);
+                pass(No{}, No{}, Yes{}, g - 1);
+            }
+        }
+        exchange(K);
+        pass(Yes{}, No{}, Yes{}, K - 1);
     }
-    exchange(K);
-    pass(Yes{}, No{}, K - 1);
-    if constexpr (COUNT) {
+    if constexpr (COUNT) {  // the generations not flushed yet
         lds_barrier();
-        for (int j = w; j < K; j += W) {
-            uint32_t acc[1] = {cnt_lds[j][lane]};
-            flush_counts<1>(acc, j, lane, group, slots);
+        if constexpr (2 * S <= K) {
+            if (w == ((K & 1) ? 0 : W - 1)) {  // K - 1 (K - 2 went in exchange(K))
+                uint32_t acc[1] = {cnt_lds[K - 1][lane]};
+                flush_counts<1>(acc, K - 1, lane, group, slots);
+            }
+        } else {
+            for (int j = w; j < K; j += W) {
+                uint32_t acc[1] = {cnt_lds[j][lane]};
+                flush_counts<1>(acc, j, lane, group, slots);
+            }
         }
     }
 }
@@ -434,7 +490,8 @@ hipError_t launch_slab_kws(const uint32_t *in, uint32_t *out, const StencilParam
     X(8, 8, 4, 4) X(8, 8, 8, 4) X(8, 16, 4, 4) X(8, 16, 8, 4) X(12, 8, 8, 4) X(12, 16, 4, 4) \
     X(12, 16, 8, 4) X(16, 8, 8, 4) X(16, 8, 10, 4) X(16, 8, 11, 4) X(16, 8, 12, 4) X(16, 8, 13, 4) \
     X(16, 8, 14, 4) X(16, 8, 16, 4) X(16, 8, 20, 4) X(16, 8, 24, 4) X(16, 16, 4, 4) X(16, 16, 6, 4) \
-    X(16, 16, 8, 4) X(16, 16, 16, 4) X(16, 4, 16, 4) X(16, 4, 24, 4) X(16, 8, 12, 2) X(16, 8, 12, 3)
+    X(16, 16, 8, 4) X(16, 16, 16, 4) X(16, 4, 16, 4) X(16, 4, 24, 4) X(16, 8, 12, 2) X(16, 8, 12, 3) \
+    X(16, 12, 8, 2) X(16, 12, 8, 4)
 
 bool stencil_slab_supported(int K, int W, int S, int NC) {
 #define GOLHIP_X(KK, WW, SS, NN) \
