@@ -281,7 +281,7 @@ def configs_leg() -> dict:
     lines = (GOLDEN / gold["cfg2"]["counts_csv"]).read_text().split()[1:]
     exp2 = np.array([int(ln.split(",")[1]) for ln in lines], dtype=np.uint64)
     with golhip.Engine(5120, 5120, k=16) as e:
-        kind = e.launch_kind(16)
+        kind = e.launch_kind(16, counts=True)
         runs, ok = [], True
         for _ in range(5):
             e.init_random(2)
@@ -304,7 +304,7 @@ def configs_leg() -> dict:
     deltas = np.load(GOLDEN / gold["cfg5"]["counts_1e6_npz"])["deltas"]
     exp5 = (int((b == 255).sum()) + np.cumsum(deltas.astype(np.int64))).astype(np.uint64)
     with golhip.Engine(4096, 4096, k=16) as e:
-        kind = e.launch_kind(16)
+        kind = e.launch_kind(16, counts=True)
         e.load(b)
         e.step(4096, counts=True)  # capture the count graphs
         e.load(b)

@@ -463,7 +463,7 @@ struct RegKernel {
     int T = 0, W = 0, S = 0, NC = 4;
     int out_rows() const { return T; }  // output rows per tile / slab
 };
-RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K) {
+RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K, bool counting) {
     RegKernel rk;
     if (!golhip::variant_is_production_family(h->variant) || h->split) return rk;
     // an explicit level split or band height (tests, tuning) asks for the streaming kernels
@@ -488,8 +488,13 @@ RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K) {
     // -- 1.33 us per turn with counts vs 1.62 for the level split, 1.21 vs 1.35 at 4096^2, 2.45
     // vs 2.87 at 8192^2), on boards where the streaming kernel has fewer than four minimal-band
     // waves per SIMD
-    // (2 row chains per wave at 8 x 12: 1 % over 4, fewer segment-start sums)
-    const int W = 8, S = K == 16 ? 12 : 8, NC = K == 16 ? 2 : 4;
+    // (2 row chains per wave at 8 x 12: 1 % over 4, fewer segment-start sums).  Counting
+    // launches at K = 16 take 12 waves x 8 rows: its four pure-halo waves (2S <= K) skip the
+    // counts and flush the other waves' per-generation sums during the launch (5120^2 with every
+    // count 1.005 -> 0.998 us/turn, 4096^2 0.951 -> 0.939; without counts 8 x 12 stays faster,
+    // 0.814 vs 0.848: profiles/r02/r02ab_slab_shapes.txt)
+    const int W = K == 16 && counting ? 12 : 8;
+    const int S = K == 16 ? (counting ? 8 : 12) : 8, NC = K == 16 ? 2 : 4;
     if (!golhip::stencil_slab_supported(K, W, S, NC)) return rk;
     const int64_t per = golhip::chunk_words(K, h->variant);
     const int64_t nchunks = (h->wd + per - 1) / per;
@@ -519,7 +524,7 @@ int64_t max_band_rows(golhip_t h) {
 hipError_t launch_auto(golhip_t h, int K, const uint32_t *in, uint32_t *out,
                        const StencilParams &p, unsigned long long *slots, hipStream_t s) {
     const int64_t rows_total = (p.r0e - p.r0b) + (p.r1e - p.r1b);
-    if (const RegKernel rk = pick_reg_kernel(h, rows_total, K); rk.kind) {
+    if (const RegKernel rk = pick_reg_kernel(h, rows_total, K, slots != nullptr); rk.kind) {
         StencilParams q = p;
         const int T = rk.out_rows();
         q.band = T;
@@ -1559,12 +1564,16 @@ int golhip_checkpoint_load(golhip_t h, const char *path) {
 }
 
 int golhip_launch_kind(golhip_t h, int k, int *kind, int *param) {
+    return golhip_launch_kind_counts(h, k, 0, kind, param);
+}
+
+int golhip_launch_kind_counts(golhip_t h, int k, int counting, int *kind, int *param) {
     if (!h || !kind || !param || k < 1 || k > golhip::kMaxK) return GOLHIP_ERR_ARG;
     *kind = 0;
     *param = 0;
     if (h->split) return GOLHIP_OK;  // strips: the streaming kernel around the halo exchange
     const int64_t rows = h->shards[0].rows;
-    if (const RegKernel rk = pick_reg_kernel(h, rows, k); rk.kind) {
+    if (const RegKernel rk = pick_reg_kernel(h, rows, k, counting != 0); rk.kind) {
         *kind = rk.kind;
         *param = rk.kind == 2 ? rk.T : (rk.NC != 4 ? rk.NC * 10000 : 0) + rk.W * 100 + rk.S;
     } else if (const int S = pick_split(h, rows, k); S > 1) {

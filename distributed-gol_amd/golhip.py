@@ -39,7 +39,7 @@ EXPORTS = [
     "golhip_store_bytes", "golhip_store_words", "golhip_load_words", "golhip_step",
     "golhip_alive_count", "golhip_alive_cells", "golhip_flips", "golhip_turn",
     "golhip_set_turn", "golhip_set_k", "golhip_set_band_rows", "golhip_sync", "golhip_timing",
-    "golhip_kernel_time", "golhip_launch_plan", "golhip_launch_kind", "golhip_set_fixed_k", "golhip_track_flips",
+    "golhip_kernel_time", "golhip_launch_plan", "golhip_launch_kind", "golhip_launch_kind_counts", "golhip_set_fixed_k", "golhip_track_flips",
     "golhip_step_flips", "golhip_flips_ring_capacity", "golhip_flips_fetch",
     "golhip_checkpoint_save", "golhip_checkpoint_load", "golhip_checkpoint_info",
 ]
@@ -123,6 +123,8 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
         "golhip_launch_plan": ([i64, i64, i32, i32, i64, ctypes.c_void_p, ctypes.c_size_t,
                                 ctypes.POINTER(ctypes.c_size_t)], i32),
         "golhip_launch_kind": ([H, i32, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], i32),
+        "golhip_launch_kind_counts": ([H, i32, i32, ctypes.POINTER(ctypes.c_int),
+                                       ctypes.POINTER(ctypes.c_int)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -393,11 +395,12 @@ class Engine:
         self._check(self._L.golhip_set_band_rows(self._h, rows))
         self.info = self.get_info()
 
-    def launch_kind(self, k: int) -> tuple[str, int]:
-        """The kernel a k-deep launch runs: ("stream", 0), ("split", S), ("tile", T) or
-        ("slab", 100 W + S)."""
+    def launch_kind(self, k: int, counts: bool = False) -> tuple[str, int]:
+        """The kernel a k-deep launch runs (with / without per-generation counts): ("stream", 0),
+        ("split", S), ("tile", T) or ("slab", [10000 NC +] 100 W + S)."""
         kind, param = ctypes.c_int(), ctypes.c_int()
-        self._check(self._L.golhip_launch_kind(self._h, k, ctypes.byref(kind), ctypes.byref(param)))
+        self._check(self._L.golhip_launch_kind_counts(self._h, k, int(counts), ctypes.byref(kind),
+                                                      ctypes.byref(param)))
         return ("stream", "split", "tile", "slab")[kind.value], param.value
 
     def sync(self):

@@ -185,8 +185,12 @@ int golhip_set_band_rows(golhip_t h, int band_rows); /* 0 = automatic */
 /* Which kernel a k-deep launch on this handle's first strip runs: *kind = 0 the streaming kernel
  * (gol_stencil, gol_step1 at k = 1), 1 the level-split kernel (*param = waves per band), 2 the
  * register-tile kernel gol_tile (*param = tile height T), 3 the register-slab kernel gol_slab
- * (*param = 100 * waves + rows per wave).  Introspection for tests and the bench line. */
+ * (*param = [10000 * row chains +] 100 * waves + rows per wave).  Introspection for tests and the
+ * bench line.  golhip_launch_kind describes a launch without per-generation counts,
+ * golhip_launch_kind_counts one with (counting != 0) or without them: small boards pick a
+ * different slab shape when counting. */
 int golhip_launch_kind(golhip_t h, int k, int *kind, int *param);
+int golhip_launch_kind_counts(golhip_t h, int k, int counting, int *kind, int *param);
 int golhip_sync(golhip_t h);                         /* wait for all queued device work */
 /* HIP-event timing of golhip_step calls on the handle's first strip (one event pair per call
  * around its back-to-back stencil launches); kernel_time reports the summed span, the number of

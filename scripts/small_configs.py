@@ -24,7 +24,7 @@ res = {}
 lines = (GOLDEN / gold["cfg2"]["counts_csv"]).read_text().split()[1:]
 exp2 = np.array([int(ln.split(",")[1]) for ln in lines], dtype=np.uint64)
 with golhip.Engine(5120, 5120, k=16) as e:
-    kind = e.launch_kind(16)
+    kind = e.launch_kind(16, counts=True)
     runs = []
     for _ in range(3):
         e.init_random(2)
@@ -46,7 +46,7 @@ golhip.place(b, golhip.parse_rle((GOLDEN / "r_pentomino.rle").read_text()), 2048
 deltas = np.load(GOLDEN / gold["cfg5"]["counts_1e6_npz"])["deltas"]
 exp5 = (int((b == 255).sum()) + np.cumsum(deltas.astype(np.int64))).astype(np.uint64)
 with golhip.Engine(4096, 4096, k=16) as e:
-    kind = e.launch_kind(16)
+    kind = e.launch_kind(16, counts=True)
     e.load(b)
     e.sync()
     t = time.perf_counter()

@@ -477,7 +477,9 @@ def test_small_board_picks_register_slab(golhip, oracle):
     words = oracle.init_random(5120, 512, seed=2)
     with golhip.Engine(5120, 512, k=16) as e:
         assert e.launch_kind(16) == ("slab", 20812)
+        assert e.launch_kind(16, counts=True) == ("slab", 21208)
         assert e.launch_kind(8) == ("slab", 808)
+        assert e.launch_kind(8, counts=True) == ("slab", 808)
         e.load_words(words)
         counts = e.step(200, counts=True)
         got = e.store_words()
