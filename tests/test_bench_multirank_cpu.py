@@ -1,0 +1,152 @@
+"""bench.py's N > 1 control flow on CPU: two gloo ranks run bench.main() exactly as
+`torch.distributed.run --nproc-per-node 2 bench.py --gpus 2 ...` would, with the GPU engine
+replaced by a host stand-in that records every step call.  The driver's 8-GPU scaling run is the
+only place the rank path meets hardware, so this checks what can break there without a GPU:
+every rank makes the same collective calls in the same order (barriers, the max-over-ranks
+timing, the pre-heat turn count taken from the cold pass), no N == 1-only leg runs, and rank 0
+prints one well-formed JSON line with the whole-job value.
+
+The stand-in does no Life arithmetic (the GPU tests cover that); it sleeps in proportion to the
+cells a step updates so the timing path sees plausible numbers.
+"""
+import json
+import os
+import socket
+import sys
+import time
+
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import PKG, ROOT
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class _Info:
+    def __init__(self, rows):
+        self.rows = rows
+
+
+class FakeEngine:
+    """Host stand-in for golhip.Engine in rank mode (the calls bench.py makes)."""
+
+    log = []
+
+    def __init__(self, width, height, ngpus=1, k=1, *, rank=None, world_size=None, device=0,
+                 nccl_id=None):
+        import golhip
+
+        assert world_size and world_size > 1 and nccl_id is not None and len(nccl_id) > 0
+        y0, rows = golhip.strip_bounds(height, world_size, rank)
+        self.width, self.rows, self.k = width, rows, k
+        self.info = _Info(rows)
+        self.turn = 0
+        self.timed = False
+        self.t_ms = 0.0
+        self.launches = 0
+        self.gens = 0
+        FakeEngine.log.append(("create", width, height, rank, world_size))
+
+    def init_random(self, seed):
+        self.turn = 0
+        FakeEngine.log.append(("init", seed))
+
+    def set_band_rows(self, n):
+        pass
+
+    def step(self, turns, counts=False):
+        assert not counts
+        dt = self.width * self.rows * turns / 5e13  # ~50 TCUPS worth of sleeping
+        time.sleep(dt)
+        if self.timed:
+            self.t_ms += dt * 1e3
+            self.launches += -(-turns // self.k)
+            self.gens += turns
+        self.turn += turns
+        FakeEngine.log.append(("step", turns))
+
+    def sync(self):
+        pass
+
+    def timing(self, enable):
+        self.timed = bool(enable)
+
+    def kernel_time(self):
+        return self.t_ms, self.launches, self.gens
+
+    def alive_count(self):
+        import torch
+        import torch.distributed as dist
+
+        t = torch.tensor([1000 + self.turn], dtype=torch.int64)  # collective, like the RCCL sum
+        dist.all_reduce(t)
+        return int(t.item())
+
+    def close(self):
+        FakeEngine.log.append(("close",))
+
+
+def _worker(rank, world, port, out_dir):
+    for p in (str(ROOT), str(ROOT / "oracle"), str(PKG)):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch
+
+    torch.cuda.set_device = lambda d: None
+    torch.cuda.synchronize = lambda *a, **k: None
+    import golhip
+
+    golhip.Engine = FakeEngine
+    golhip.nccl_unique_id = lambda: b"x" * 128
+    import bench
+
+    sys.argv = ["bench.py", "--gpus", str(world), "--steps", "20", "--warmup", "5",
+                "--size", "4096", "--strong-size", "2048", "--strong-steps", "32",
+                "--preheat-ms", "50"]
+    out = os.path.join(out_dir, f"rank{rank}.out")
+    with open(out, "w") as f:
+        so = sys.stdout
+        sys.stdout = f
+        try:
+            bench.main()
+        finally:
+            sys.stdout = so
+    with open(os.path.join(out_dir, f"rank{rank}.log"), "w") as f:
+        json.dump(FakeEngine.log, f)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_rank_path_cpu(tmp_path, world):
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    logs = [json.loads((tmp_path / f"rank{r}.log").read_text()) for r in range(world)]
+    # every rank issued the same sequence of engine calls (step sizes included): the pre-heat
+    # turn count is the same everywhere, so the RCCL exchanges of the real engine would pair up
+    steps = [[e for e in log if e[0] in ("step", "init", "close")] for log in logs]
+    assert all(s == steps[0] for s in steps[1:])
+    creates = [[e for e in log if e[0] == "create"] for log in logs]
+    assert [c[0][3] for c in creates] == list(range(world))  # one engine per rank, its own strip
+    assert all(len(c) == 2 for c in creates)  # the weak-scaling board and the 262144^2-style leg
+    # rank 0 prints exactly one JSON line, the others nothing
+    out0 = (tmp_path / "rank0.out").read_text().strip().splitlines()
+    assert len(out0) == 1
+    for r in range(1, world):
+        assert (tmp_path / f"rank{r}.out").read_text().strip() == ""
+    line = json.loads(out0[0])
+    assert line["n_gpus"] == world and line["steps"] == 20 and line["warmup"] == 5
+    assert line["config"]["height"] == 4096 * world and line["config"]["parallelism"] == f"rows{world}"
+    assert line["scaling"] == "weak" and line["value"] > 0
+    # N > 1: no k sweep, configs leg, flips leg or CPU baseline; pre-heat ran after a cold pass
+    assert line["k_sweep_gcups"] is None and line["configs"] is None
+    assert line["flips_path"] is None and line["cpu_baseline"] is None
+    assert line["cold_start"]["preheat_turns"] >= 16
+    assert line["strong_262144"]["rows_per_gpu"] == -(-2048 // world)
