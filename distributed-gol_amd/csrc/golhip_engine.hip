@@ -293,33 +293,39 @@ int pick_k(int n) {
     return kk;
 }
 
-// Measured throughput of a K-generation launch of the production variant, T cell-updates/s at
-// 65536^2: the mean of the two fixed-depth k sweeps of profiles/r02/bench_sweeps.json (one
-// process each; runs differ by up to 5 %, so depths 12-16 are a near tie and K = 16 keeps the
-// bulk; 6 interpolated), and the fixed cost of one launch (kernel boundary + the last round's
-// drain, us).
-double launch_rate_tcups(int K) {
+// Measured throughput of a K-generation launch of the production variant, T cell-updates/s, on a
+// pre-heated chip (profiles/r02/r02ad_bulk_depth.txt and the k sweeps of the round-2 bench lines:
+// 65536^2, 256+ generations per depth; 6 interpolated), and the fixed cost of one launch (kernel
+// boundary + the last round's drain, us).  Boards of >= 2^35 cells per strip have their own
+// ranking: at 262144^2 (2096-row bands) K = 16 runs 129 vs 122 at K = 12, while every smaller
+// streaming board measured runs K = 12 faster (16384^2 +17 %, 32768^2 +9.5 %, 65536^2 +2.3 %,
+// 131072^2 +3 %: r02ae/r02af).  Only the ranking and the ratios matter to the planner.
+constexpr double kLargeStripCells = 34359738368.0;  // 2^35
+double launch_rate_tcups(int K, double cells = 0.0) {
+    const bool large = cells >= kLargeStripCells;
     switch (K) {
-        case 1: return 21.6;
-        case 2: return 33.8;
-        case 4: return 63.0;
-        case 6: return 85.0;
-        case 8: return 106.4;
-        case 10: return 111.2;
-        case 12: return 114.9;
-        case 14: return 114.0;
-        case 16: return 117.9;
+        case 1: return 22.8;
+        case 2: return 35.4;
+        case 4: return 68.4;
+        case 6: return 92.0;
+        case 8: return 115.4;
+        case 10: return 116.7;  // 120.9 on sparse boards; 20 turns as 10 + 10 ran 97.7 TCUPS vs 111.8 as 12 + 8
+        case 12: return large ? 122.0 : 123.6;
+        case 14: return large ? 125.0 : 122.1;
+        case 16: return large ? 129.0 : 120.2;
         case 32: return 100.9;
         default: return 50.0;
     }
 }
 
 // The depth <= kmax with the highest measured rate: the bulk depth of long runs (k is the maximum
-// depth; deeper is not always faster -- 12 and 14 keep 5 waves per SIMD, 16 keeps 4).
-int best_rate_k(int kmax) {
+// depth; deeper is not always faster -- 12 and 14 keep 5 waves per SIMD, 16 keeps 4, and the
+// band trapezoid of a K-deep launch grows with K).
+int best_rate_k(int kmax, double cells) {
     int best = 1;
     for (int K = 1; K <= kmax; ++K)
-        if (golhip::stencil_k_supported(K) && launch_rate_tcups(K) > launch_rate_tcups(best)) best = K;
+        if (golhip::stencil_k_supported(K) && launch_rate_tcups(K, cells) > launch_rate_tcups(best, cells))
+            best = K;
     return best;
 }
 constexpr double kLaunchOverheadUs = 4.0;
@@ -337,7 +343,7 @@ int plan_first_k(int64_t n, int kmax, double cells) {
     for (int m = 1; m <= N; ++m)
         for (int K : {32, 16, 14, 12, 10, 8, 6, 4, 2, 1}) {
             if (K > m || K > kmax || !golhip::stencil_k_supported(K)) continue;
-            const double c = best[m - K] + cells * K / (launch_rate_tcups(K) * 1e6) + kLaunchOverheadUs;
+            const double c = best[m - K] + cells * K / (launch_rate_tcups(K, cells) * 1e6) + kLaunchOverheadUs;
             if (c < best[m]) {
                 best[m] = c;
                 first[m] = K;
@@ -901,13 +907,21 @@ struct LaunchPlanner {
     bool graphs;
     int64_t left;
     bool keep_last;  // the last generation is always a plain launch (it writes the flips)
+    // k: the maximum depth; Kfull: the deepest depth used (graph replays), pick_k(k) unless the
+    // streaming kernel's bulk depth is capped (stream_depth_cap); Kbulk: the bulk depth of long
+    // runs without graphs
+    // stream: the board runs the streaming kernel (no register slab/tile, no level split): its
+    // graph replays use the best-rate depth too (16384^2: 64.5 vs 55.3 TCUPS at K = 12 vs 16,
+    // profiles/r02/r02ae_depth_by_size.txt); the register kernels are tuned at the full depth
     LaunchPlanner(double cells_, int k, int64_t turns, bool small, bool fixed = false,
-                  bool keep_last_ = false, int window = 4096)
-        : cells(cells_), Kfull(pick_k(k)), left(turns), keep_last(keep_last_) {
+                  bool keep_last_ = false, int window = 4096, bool stream = false)
+        : cells(cells_),
+          Kfull(small && stream && !fixed ? best_rate_k(pick_k(k), cells_) : pick_k(k)),
+          left(turns), keep_last(keep_last_) {
         M = std::max(2, (kGraphGens / Kfull) & ~1);
         Mbig = std::max(M, (std::min(kGraphGensBig, window) / Kfull) & ~1);
         graphs = small && turns >= (int64_t)M * Kfull + (keep_last ? 1 : 0);
-        Kbulk = small || fixed ? Kfull : best_rate_k(Kfull);
+        Kbulk = small || fixed ? Kfull : best_rate_k(Kfull, cells);
     }
     int next() {
         for (int m : {Mbig, M})
@@ -1259,9 +1273,14 @@ static int run_steps(golhip_t h, int64_t turns, uint64_t *alive_per_turn, bool r
         if (rc) return rc;
     }
     int64_t done = 0;
-    LaunchPlanner plan((double)h->L * (double)h->height, ring ? 1 : h->k, turns,
-                       !ring && graph_worthy(h, pick_k(h->k)), h->fixed_k || ring, h->track_flips,
-                       h->count_window);
+    const int kmax = pick_k(h->k);
+    const bool stream = !ring && h->shards.size() == 1 &&
+                        pick_reg_kernel(h, h->shards[0].rows, kmax, counting).kind == 0 &&
+                        pick_split(h, h->shards[0].rows, kmax) <= 1;
+    // planned per strip: the band geometry and each GPU's launch time follow the strip
+    LaunchPlanner plan((double)h->L * (double)h->shards[0].rows, ring ? 1 : h->k, turns,
+                       !ring && graph_worthy(h, kmax), h->fixed_k || ring, h->track_flips,
+                       h->count_window, stream);
     const int Kfull = plan.Kfull;
     int64_t win = 0;  // generations pending in the count window, from turn offset done - win
     while (done < turns) {
@@ -1589,7 +1608,16 @@ int golhip_launch_plan(int64_t width, int64_t height, int strips, int k, int64_t
         return GOLHIP_ERR_ARG;
     const double cells = (double)lcm64(width, 128) * (double)height;
     const int Kfull = pick_k(k);
-    LaunchPlanner plan(cells, k, turns, strips == 1 && small_board(cells, Kfull));
+    // the engine's automatic choice for one strip: the register slab where the streaming kernel
+    // would have at most 16 minimal-band waves per CU (256 CUs), else streaming (pick_reg_kernel)
+    const int64_t wd = lcm64(width, 128) / 32;
+    const int64_t per = golhip::chunk_words(Kfull, golhip::kVariantProd);
+    const int64_t waves1 = (height + std::max(Kfull, 8) - 1) / std::max(Kfull, 8) * ((wd + per - 1) / per);
+    const bool stream = strips > 1 || !golhip::stencil_slab_supported(Kfull, 8, Kfull == 16 ? 12 : 8,
+                                                                       Kfull == 16 ? 2 : 4) ||
+                        waves1 > 16 * 256;
+    LaunchPlanner plan(cells / strips, k, turns, strips == 1 && small_board(cells, Kfull), false, false,
+                       4096, stream);
     size_t cnt = 0;
     while (plan.left > 0) {
         const int K = plan.next();
