@@ -294,7 +294,10 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
     __shared__ uint32_t ex[2][W][2][64];
     // per-generation alive counts of the slab, per lane (summed over the waves by LDS adds; one
     // global atomic per generation per slab at the end)
-    __shared__ uint32_t cnt_lds[COUNT ? K : 1][64];
+    // per-generation alive counts, one slot per wave and lane (plain LDS stores; twelve waves'
+    // atomic adds to ONE slot per lane serialised in the LDS pipe in front of every barrier),
+    // summed over the waves by the flushing wave
+    __shared__ uint32_t cnt_lds[COUNT ? K : 1][COUNT ? W : 1][64];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     // XCD-aware order: the dispatcher deals workgroups round-robin over the 8 XCDs (each with its
@@ -328,10 +331,16 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
     // slab row of c[1]: output row o = w*S + (r - 1) - K is this band's if 0 <= o < nrows
     const int o0 = w * S - K;
     if constexpr (COUNT)
-        for (int j = w; j < K; j += W) cnt_lds[j][lane] = 0;
+        for (int j = 0; j < K; ++j) cnt_lds[j][w][lane] = 0;  // halo waves never write theirs
     // LDS-only barrier: the waves' global stores and count atomics stay in flight (a
     // __syncthreads() would also drain vmcnt every generation)
     auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    auto cnt_sum = [&](int j) {
+        uint32_t a = 0;
+#pragma unroll
+        for (int ww = 0; ww < W; ++ww) a += cnt_lds[j][ww][lane];
+        return a;
+    };
     auto exchange = [&](int g) {
         const int par = g & 1;
         ex[par][w][0][lane] = c[1];
@@ -348,7 +357,7 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
             // K = 16 the same scheme is slower than the end flush, and so is letting the two
             // waves flush in batches once idle: profiles/r02/r02aa_slab_flush.txt.)
             if (g >= 2 && w == ((g & 1) ? W - 1 : 0)) {
-                uint32_t acc[1] = {cnt_lds[g - 2][lane]};
+                uint32_t acc[1] = {cnt_sum(g - 2)};
                 flush_counts<1>(acc, g - 2, lane, group, slots);
             }
         }
@@ -384,8 +393,7 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
             }
         });
         if constexpr (CNT)
-            if (count_lane) __hip_atomic_fetch_add(&cnt_lds[gen][lane], cnt, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+            cnt_lds[gen][w][lane] = count_lane ? cnt : 0u;
     };
     using No = std::false_type;
     using Yes = std::true_type;
@@ -434,12 +442,12 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
         lds_barrier();
         if constexpr (2 * S <= K) {
             if (w == ((K & 1) ? 0 : W - 1)) {  // K - 1 (K - 2 went in exchange(K))
-                uint32_t acc[1] = {cnt_lds[K - 1][lane]};
+                uint32_t acc[1] = {cnt_sum(K - 1)};
                 flush_counts<1>(acc, K - 1, lane, group, slots);
             }
         } else {
             for (int j = w; j < K; j += W) {
-                uint32_t acc[1] = {cnt_lds[j][lane]};
+                uint32_t acc[1] = {cnt_sum(j)};
                 flush_counts<1>(acc, j, lane, group, slots);
             }
         }
