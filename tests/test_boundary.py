@@ -108,3 +108,23 @@ def test_launch_plan_long_runs_replay_large_graphs(golhip):
     graphs = [-d for d in plan if d < 0]
     assert graphs[:2] == [4096] * 2 and set(graphs[2:]) <= {128}
     assert sum(graphs) + sum(d for d in plan if d > 0) == 10000
+
+
+def test_launch_plan_bulk_depth_by_board_size(golhip):
+    """The bulk depth follows the strip size (profiles/r02/r02ae_depth_by_size.txt, pre-heated
+    chip): K = 12 on streaming boards below 2^35 cells per strip (5 resident waves per SIMD, an
+    11-row band trapezoid), K = 16 on larger strips (262144^2: 129 vs 122 TCUPS); small streaming
+    boards replay graphs of 12-deep launches, register-slab boards of 16-deep ones."""
+    from collections import Counter
+
+    assert Counter(golhip.launch_plan(65536, 65536, 16, 1008)) == {12: 84}
+    assert Counter(golhip.launch_plan(131072, 131072, 16, 480)) == {12: 40}
+    assert Counter(golhip.launch_plan(262144, 262144, 16, 160)) == {16: 10}
+    # per strip: the 262144^2 board over 8 ranks is 2^33 cells per strip -> K = 12
+    assert set(golhip.launch_plan(262144, 262144, 16, 480, strips=8)) == {12}
+    graphs16k = [-d for d in golhip.launch_plan(16384, 16384, 16, 2000) if d < 0]
+    assert graphs16k and set(graphs16k) == {120}  # 10 launches of K = 12 per replay
+    graphs5k = [-d for d in golhip.launch_plan(5120, 5120, 16, 10000) if d < 0]
+    assert graphs5k[:2] == [4096, 4096]  # the register slab keeps K = 16
+    # the maximum depth still caps everything
+    assert max(golhip.launch_plan(65536, 65536, 8, 1000)) <= 8
