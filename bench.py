@@ -406,12 +406,19 @@ def main():
     words_per_launch = local_cells / 32 * gens_per_launch
     valu_alg = words_per_launch / 64 * VALU_PER_WORD_GEN
     valu_achieved = valu_alg / (avg_launch_ms * 1e-3) / 1e12
-    pmc_entry = {}
+    pmc_entry, pmc = {}, {}
     try:
         pmc = json.loads(Path(a.pmc_file).read_text())
         pmc_entry = pmc.get(f"{width}x{eng.info.rows}_k{dominant_k}", {})
     except Exception:
         pass
+    # PMC-issued VALU instructions of the whole timed region, when every depth it ran has a PMC
+    # entry for this board (profiles/pmc_traffic.json): sum over launches / the region's kernel time
+    issued_all = None
+    per_depth = [pmc.get(f"{width}x{eng.info.rows}_k{d}", {}).get("valu_instr_per_launch")
+                 for d in depth_count]
+    if depth_count and all(per_depth) and kern_ms > 0 and not a.no_timing:
+        issued_all = sum(v * depth_count[d] for v, d in zip(per_depth, depth_count))
     traffic = pmc_entry.get("hbm_bytes_per_launch")
     uniform = len(depth_count) == 1  # every timed launch ran the same depth
     issued = pmc_entry.get("valu_instr_per_launch")
@@ -433,6 +440,10 @@ def main():
             if uniform:
                 roof["issued_pmc"] = round(issued / (avg_launch_ms * 1e-3) / 1e12, 4)
                 roof["issued_frac"] = round(issued / (avg_launch_ms * 1e-3) / 1e12 / VALU_PEAK_T, 4)
+        if issued_all and not uniform:
+            # mixed depths (e.g. 82 x K=12 + 1 x K=16): every launch's PMC count over the region
+            roof["issued_pmc"] = round(issued_all / (kern_ms * 1e-3) / 1e12, 4)
+            roof["issued_frac"] = round(issued_all / (kern_ms * 1e-3) / 1e12 / VALU_PEAK_T, 4)
         if pmc_entry.get("clock_ghz"):
             roof["clock_ghz_pmc"] = pmc_entry["clock_ghz"]
     roof.update({"kernel": kernel_name, "avg_launch_us": round(avg_launch_ms * 1e3, 2),
