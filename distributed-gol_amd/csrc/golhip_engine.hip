@@ -1723,6 +1723,17 @@ int golhip_timing(golhip_t h, int enable) {
     h->tms = 0.0;
     h->tlaunches = 0;
     h->tgens = 0;
+    // create the event pairs now: a hipEventCreate inside the first timed golhip_step call would
+    // add its host cost to a caller's timed region (a 20-turn region is ~0.75 ms)
+    if (h->timing) {
+        HIPCHK(h, hipSetDevice(h->shards[0].device));
+        while (h->tpool.size() < 4) {
+            TimingPair tp;
+            HIPCHK(h, hipEventCreate(&tp.a));
+            HIPCHK(h, hipEventCreate(&tp.b));
+            h->tpool.push_back(tp);
+        }
+    }
     return GOLHIP_OK;
 }
 
