@@ -113,11 +113,15 @@ def timed_steps(eng: golhip.Engine, steps: int, world: int) -> float:
     eng.sync()
     t0 = time.perf_counter()
     eng.step(steps)
-    eng.sync()
+    # torch.cuda.synchronize() is hipDeviceSynchronize: it waits for EVERY stream of the device,
+    # the engine's own compute/edge/comm streams included (checked: the wall time never undercuts
+    # the engine's HIP-event span, profiles/r02/r02am_timed_region_host.txt); a golhip_sync of the
+    # three engine streams before it only added ~10 us of host round trips to a 20-turn region
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    eng.sync()
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -391,6 +395,9 @@ def main():
         launches = -(-a.steps // a.k)
         kern_ms, gens = dt * 1e3, a.steps
 
+    if not a.no_timing and kern_ms > dt * 1e3 * 1.001:
+        raise SystemExit(f"timed region {dt * 1e3:.3f} ms shorter than the engine's event span "
+                         f"{kern_ms:.3f} ms: the end-of-region synchronisation missed engine work")
     total_updates = width * height * a.steps
     gcups = total_updates / dt / 1e9
     ms_per_step = dt * 1e3 / a.steps
