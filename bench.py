@@ -88,6 +88,9 @@ def parse():
     ap.add_argument("--no-sweep", action="store_true", help="skip the k sweep")
     ap.add_argument("--cpu-size", type=int, default=65536, help="CPU baseline board (the bench board)")
     ap.add_argument("--cpu-turns", type=int, default=2, help="CPU baseline turns (~15 s of CPU work)")
+    ap.add_argument("--cpu-threads-per-server", type=int, default=0,
+                    help="goroutine-threads per reference server in the CPU baseline "
+                         "(0 = ceil(host CPUs / 4): every host core)")
     ap.add_argument("--no-timing", action="store_true",
                     help="no per-launch HIP events in the timed region (roofline from wall time)")
     ap.add_argument("--pmc-file", default=str(ROOT / "profiles" / "pmc_traffic.json"))
@@ -142,22 +145,40 @@ def host_cpu() -> tuple[int, str]:
     return os.cpu_count() or 0, model
 
 
-def cpu_baseline(size: int, turns: int, threads_per_server: int) -> dict:
+def cpu_share() -> dict:
+    """What this process may actually run on: its CPU affinity and the cgroup CPU quota (a GPU box
+    shares the host: os.cpu_count() shows every CPU of the machine, the quota what this job gets)."""
+    out = {"affinity_cpus": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
+           "cgroup_cpu_quota": None}
+    try:
+        quota, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if quota != "max":
+            out["cgroup_cpu_quota"] = round(int(quota) / int(period), 2)
+    except (OSError, ValueError):
+        pass
+    return out
+
+
+def cpu_baseline(size: int, turns: int, threads_per_server: int | None = None) -> dict:
     """The reference's algorithm (oracle/gol_oracle.c oracle_ref_*), timed on this host.
 
     Sample: `turns` turns of the bench board itself (65536^2 random, seed 3) with the reference's
     cost structure -- byte cells, branchy torus wrap + /255, fresh rows per turn, 4 broker strips
     x `threads_per_server` goroutine-threads, a private full-world copy per server per turn (the
-    gob fan-out of broker/broker.go:51,64) and the controller's per-turn alive scan
-    (gol/distributor.go:186).  The RPC transport itself (gob encode/TCP) is not timed.  Plus
-    configs[0] in full: images/512x512.pgm for 100 turns, checked byte-exact against the
-    reference's check/images/512x512x100.pgm."""
+    gob fan-out of broker/broker.go:51,64; each server copies its own, concurrently)
+    and the controller's per-turn alive scan (gol/distributor.go:186).  The RPC transport itself
+    (gob encode/TCP) is not timed.  threads_per_server defaults to ceil(host CPUs / 4): T = every
+    host core (each reference server runs req.Threads goroutines,
+    server/server.go:83-97).  Plus configs[0] in full: images/512x512.pgm for 100 turns, checked
+    byte-exact against the reference's check/images/512x512x100.pgm."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import numpy as np
 
     import oracle
 
     nproc, model = host_cpu()
+    if threads_per_server is None:
+        threads_per_server = max(1, -(-nproc // 4))
     threads = 4 * threads_per_server
     # configs[0] in full
     ref = GOLDEN / "reference"
@@ -189,6 +210,7 @@ def cpu_baseline(size: int, turns: int, threads_per_server: int) -> dict:
         "unit": "GCUPS",
         "cores": threads,
         "host_cores": nproc,
+        **cpu_share(),
         "cpu_model": model,
         "fanout_copy": True,
         "kind": "port",
@@ -196,7 +218,8 @@ def cpu_baseline(size: int, turns: int, threads_per_server: int) -> dict:
                    f"reference algorithm: byte cells, branchy torus wrap + /255, fresh rows per "
                    f"turn, 4 broker strips x {threads_per_server} goroutine-threads = {threads} OS "
                    f"threads, full-world copy per server per turn, per-turn alive scan; gob/TCP "
-                   f"transport not timed; {dt:.1f} s"),
+                   f"transport not timed; {dt:.1f} s; threads = every host CPU (os.cpu_count()), "
+                   f"which on a shared GPU box may exceed the job's CPU quota (cgroup_cpu_quota)"),
         "cfg1_512x100": {"s": round(dt512, 4), "gcups": round(512 * 512 * 100 / dt512 / 1e9, 4),
                          "bit_exact_vs_reference_fixture": bool(exact)},
         "cfg2_5120_first20": {"s": round(dt2, 4), "gcups": round(5120 * 5120 * 20 / dt2 / 1e9, 4),
@@ -206,26 +229,27 @@ def cpu_baseline(size: int, turns: int, threads_per_server: int) -> dict:
     }
 
 
-def golden_count(turn: int) -> int | None:
-    """The oracle's alive count of configs[2] (65536^2, seed 3) after `turn` turns, if pinned."""
-    path = GOLDEN / "cfg3_65536_seed3_counts.csv"
-    if turn < 1 or not path.exists():
+def golden_count(width: int, height: int, seed: int, turn: int) -> int | None:
+    """The oracle's alive count of the width x height random board (p = 0.5, `seed`) after `turn`
+    turns, if tests/golden/synthetic_golden.json registers a per-turn count CSV for that board
+    (scripts/make_golden.py: configs[1..3], and the weak-scaling boards 65536 x 65536*N for
+    N = 2, 4, 8 that bench --gpus N runs)."""
+    if turn < 1:
         return None
-    for line in path.read_text().splitlines()[1:]:
-        t, c = line.split(",")
-        if int(t) == turn:
-            return int(c)
-    return None
-
-
-def golden_count_cfg4(turn: int) -> int | None:
-    path = GOLDEN / "cfg4_262144_seed4_counts.csv"
-    if turn < 1 or not path.exists():
+    try:
+        gold = json.loads((GOLDEN / "synthetic_golden.json").read_text())
+    except OSError:
         return None
-    for line in path.read_text().splitlines()[1:]:
-        t, c = line.split(",")
-        if int(t) == turn:
-            return int(c)
+    for entry in gold.values():
+        if (entry.get("width"), entry.get("height"), entry.get("seed")) != (width, height, seed):
+            continue
+        path = GOLDEN / entry.get("counts_csv", "")
+        if not entry.get("counts_csv") or not path.exists():
+            continue
+        for line in path.read_text().splitlines()[1:]:
+            t, c = line.split(",")
+            if int(t) == turn:
+                return int(c)
     return None
 
 
@@ -335,17 +359,23 @@ def main():
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    # test hook (tests/test_gpu_rank_host.py): GOLHIP_HOST_COMM=1 runs the rank engines with the gloo
+    # host transport instead of RCCL, so N ranks can share the one GPU of a test box (RCCL refuses
+    # two ranks on one device); the engine, its launch plan and the timed region are unchanged
+    host_comm = os.environ.get("GOLHIP_HOST_COMM", "0") == "1" and world > 1
+    if host_comm:
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
 
     width = a.size
     height = a.height or a.size * world
     nccl_id = None
-    if world > 1:
+    if world > 1 and not host_comm:
         obj = [golhip.nccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         nccl_id = obj[0]
     eng = golhip.Engine(width, height, k=a.k, rank=rank, world_size=world, device=local,
-                        nccl_id=nccl_id)
+                        nccl_id=nccl_id, host_comm=golhip.GlooHostComm() if host_comm else None)
     if a.band_rows:
         eng.set_band_rows(a.band_rows)
     eng.init_random(a.seed)
@@ -461,10 +491,11 @@ def main():
                 "measured_traffic_per_launch": traffic,
                 "note": "0.25 B per cell-update; temporal blocking moves the board once per "
                         "launch, so this exceeds 1 for k > 1 and is not the binding bound"}
-    # parity: the canary against the oracle's golden count (configs[2] board, N == 1 only)
+    # parity: the canary against the oracle's golden count of this board (every registered board:
+    # configs[2] at N == 1, the weak-scaling boards 65536 x 65536*N at N = 2, 4, 8)
     parity = None
-    if world == 1 and width == 65536 and height == 65536 and a.seed == 3:
-        exp = golden_count(a.warmup + a.steps)
+    if a.seed in (2, 3, 4):
+        exp = golden_count(width, height, a.seed, a.warmup + a.steps)
         if exp is not None:
             parity = {"turn": a.warmup + a.steps, "alive": int(alive_timed), "golden": exp,
                       "ok": int(alive_timed) == exp}
@@ -503,11 +534,12 @@ def main():
     if not a.no_strong:
         n = a.strong_size
         sid = None
-        if world > 1:  # a fresh RCCL unique id per communicator
+        if world > 1 and not host_comm:  # a fresh RCCL unique id per communicator
             obj = [golhip.nccl_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)
             sid = obj[0]
-        se = golhip.Engine(n, n, k=a.k, rank=rank, world_size=world, device=local, nccl_id=sid)
+        se = golhip.Engine(n, n, k=a.k, rank=rank, world_size=world, device=local, nccl_id=sid,
+                           host_comm=golhip.GlooHostComm() if host_comm else None)
         se.init_random(4)
         se.step(a.k)
         se.sync()
@@ -520,7 +552,7 @@ def main():
                   "rows_per_gpu": -(-n // world), "gcups": round(g, 1),
                   "gcups_per_gpu": round(g / world, 1), "ms_per_step": round(t * 1e3 / a.strong_steps, 4),
                   "alive_after": int(strong_alive)}
-        exp = golden_count_cfg4(a.k + a.strong_steps) if n == 262144 else None
+        exp = golden_count(n, n, 4, a.k + a.strong_steps)
         if exp is not None:
             strong["parity"] = {"turn": a.k + a.strong_steps, "golden": exp,
                                 "ok": int(strong_alive) == exp}
@@ -560,7 +592,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu:
-        cpu = cpu_baseline(a.cpu_size, a.cpu_turns, threads_per_server=4)
+        cpu = cpu_baseline(a.cpu_size, a.cpu_turns, threads_per_server=a.cpu_threads_per_server or None)
 
     if rank == 0:
         line = {
@@ -584,6 +616,15 @@ def main():
             },
             "parity": parity,
             "preheat_ms": a.preheat_ms,
+            # every generation this process computed on the bench board before the timed region
+            # (the cold-start pass's warmup + steps, the pre-heat turns, then this pass's warmup;
+            # the board is re-initialised from the seed before the last warmup): a plain
+            # --steps 20 --warmup 5 line is measured on a warmed chip, its idle-clock figure is
+            # cold_start
+            "untimed_generations_before_value": (
+                a.warmup + (a.warmup + a.steps + cold["preheat_turns"] if cold else 0)),
+            "transport": "gloo host transport (test hook GOLHIP_HOST_COMM=1)" if host_comm else
+                         ("rccl" if world > 1 else None),
             # the same warmup + timed turns measured first, on the chip as the process found it
             # (idle clock): what a 20-turn run pays before the clock has ramped
             "cold_start": cold,

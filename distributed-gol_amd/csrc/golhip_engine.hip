@@ -64,6 +64,11 @@ struct Shard {
     int64_t ex_rows_cap = 0, ex_slots_cap = 0;
     int32_t *ex_xy = nullptr;
     size_t ex_xy_cap = 0;
+    // device staging of host transfers (PGM bytes, uint64 words, the checkpoint byte codec),
+    // allocated once at create: no host-facing call allocates or frees device memory (a hipFree
+    // synchronises the whole device, and every `s` snapshot / PGM store used to pay one)
+    uint8_t *stage = nullptr;
+    int64_t stage_bytes = 0;
 };
 
 struct TimingPair {
@@ -97,6 +102,11 @@ struct golhip_engine {
     int64_t ring_turns = 0;      // turns held in the ring by the last golhip_step_flips
     int waves_per_cu[golhip::kMaxK + 1][golhip::kNumVariants] = {};  // occupancy cache per (K, variant)
     bool rank_mode = false;
+    // golhip_create_rank_host: the caller's host transport instead of RCCL, with pinned host
+    // buffers for the 4 K-row transfers of an exchange (halo rows x pitch words each)
+    bool host_comm_on = false;
+    golhip_host_comm host_comm{};
+    void *hc_buf[4] = {nullptr, nullptr, nullptr, nullptr};
     bool split = false;  // board held as halo'd row strips (world > 1, or GOLHIP_RING_SELF)
     int force_split = 0;  // GOLHIP_SPLIT (0 = automatic)
     int force_tile = -1;  // GOLHIP_TILE: -1 automatic, 0 never, T > 0 always (tile height T)
@@ -196,6 +206,8 @@ int ensure_extract_scratch(golhip_t h, Shard &s, int64_t rows, int64_t slots) {
     return GOLHIP_OK;
 }
 
+constexpr int64_t kStageBytes = 64ll << 20;
+
 int alloc_shard(golhip_t h, Shard &s) {
     HIPCHK(h, hipSetDevice(s.device));
     HIPCHK(h, hipStreamCreateWithFlags(&s.compute, hipStreamNonBlocking));
@@ -214,6 +226,13 @@ int alloc_shard(golhip_t h, Shard &s) {
                              sizeof(unsigned long long) * h->count_window * golhip::kCountSlots,
                              s.compute));
     HIPCHK(h, hipMalloc(&s.scratch_u64, sizeof(unsigned long long) * 4));
+    // the transfer stage: the shard's whole byte board if it fits in kStageBytes, else row chunks
+    // of it (a byte row is the widest unit any transfer stages)
+    // (GOLHIP_STAGE_BYTES, read at create, shrinks it: tests force multi-chunk transfers)
+    int64_t cap = kStageBytes;
+    if (const char *e = std::getenv("GOLHIP_STAGE_BYTES")) cap = std::max<int64_t>(1, std::atoll(e));
+    s.stage_bytes = std::max<int64_t>(h->width, std::min<int64_t>(cap, s.rows * h->width));
+    HIPCHK(h, hipMalloc(&s.stage, (size_t)s.stage_bytes));
     HIPCHK(h, hipStreamSynchronize(s.compute));
     return ensure_extract_scratch(h, s, s.rows, 1);
 }
@@ -230,7 +249,7 @@ void free_shard(Shard &s) {
     if (s.scratch_u64) (void)hipFree(s.scratch_u64);
     if (s.d_counts) (void)hipFree(s.d_counts);
     for (void *q : {(void *)s.diffbuf, (void *)s.ring, (void *)s.ex_rowcounts, (void *)s.ex_offsets,
-                    (void *)s.ex_slot_counts, (void *)s.ex_xy})
+                    (void *)s.ex_slot_counts, (void *)s.ex_xy, (void *)s.stage})
         if (q) (void)hipFree(q);
     if (s.ev_ready) (void)hipEventDestroy(s.ev_ready);
     if (s.ev_halo) (void)hipEventDestroy(s.ev_halo);
@@ -239,6 +258,20 @@ void free_shard(Shard &s) {
     if (s.comm) (void)hipStreamDestroy(s.comm);
     if (s.edge) (void)hipStreamDestroy(s.edge);
     s = Shard{};
+}
+
+// Rows per strip the launch planner ranks depths by: the largest strip of the board,
+// ceil(height / strips).  Each launch of a split board exchanges K-row halos, so in rank mode every
+// rank MUST run the same depth sequence (a different K on one rank would mismatch the
+// ncclSend/ncclRecv sizes): planning from a quantity every rank shares -- not the rank's own,
+// possibly one row shorter, strip -- guarantees that (golhip_launch_plan uses the same rows).
+int64_t strip_plan_rows(int64_t height, int strips) { return (height + strips - 1) / strips; }
+int64_t plan_rows(golhip_t h) { return strip_plan_rows(h->height, h->world_size); }
+
+// Kernel variants whose launches can write a generation's flips beside their output (the
+// production drift family; gol_step1 at K = 1).  The A/B-experiment variants cannot.
+bool variant_writes_flips(int v) {
+    return v == golhip::kVariantProd || v == golhip::kVariantDriftLds || v == golhip::kVariantDrift62;
 }
 
 int validate_geometry(int width, int height, int world, int k) {
@@ -621,7 +654,26 @@ int exchange_halos(golhip_t h, int K) {
         HIPCHK(h, hipSetDevice(s.device));
         HIPCHK(h, hipEventRecord(s.ev_ready, s.compute));
     }
-    if (h->rank_mode) {
+    if (h->host_comm_on) {
+        // host transport: stage the two sends through pinned host memory (after the block that
+        // wrote them), hand the ordered plan to the caller, copy the two halos back on the comm
+        // stream; synchronous on the host (a test / fallback transport, not the RCCL fast path)
+        Shard &s = h->shards[0];
+        golhip_xfer plan[4];
+        halo_plan(h->world_size, s.rank, s.rows, K, plan);
+        uint32_t *r0 = h->row0(s, h->cur);
+        for (int i = 0; i < 4; ++i)
+            if (plan[i].kind == 0)
+                HIPCHK(h, hipMemcpyAsync(h->hc_buf[i], r0 + plan[i].row * h->pitch, bytes,
+                                         hipMemcpyDeviceToHost, s.compute));
+        HIPCHK(h, hipStreamSynchronize(s.compute));
+        if (h->host_comm.exchange(h->host_comm.ctx, plan, 4, h->hc_buf, bytes) != 0)
+            return fail(h, GOLHIP_ERR_RCCL, "host transport: exchange of %d-row halos failed", K);
+        for (int i = 0; i < 4; ++i)
+            if (plan[i].kind == 1)
+                HIPCHK(h, hipMemcpyAsync(r0 + plan[i].row * h->pitch, h->hc_buf[i], bytes,
+                                         hipMemcpyHostToDevice, s.comm));
+    } else if (h->rank_mode) {
         for (auto &s : h->shards) HIPCHK(h, hipStreamWaitEvent(s.comm, s.ev_ready, 0));
         NCCLCHK(h, ncclGroupStart());
         for (auto &s : h->shards) {
@@ -740,7 +792,7 @@ int sync_all(golhip_t h) {
 // Sum n uint64 device values over every strip of the board into host memory `out`:
 // strips of this process are summed on the host, ranks with one ncclAllReduce.
 int reduce_u64(golhip_t h, const std::vector<unsigned long long *> &bufs, size_t n, uint64_t *out) {
-    if (h->rank_mode && h->split) {
+    if (h->rank_mode && h->split && !h->host_comm_on) {
         Shard &s = h->shards[0];
         HIPCHK(h, hipSetDevice(s.device));
         NCCLCHK(h, ncclAllReduce(bufs[0], bufs[0], n, ncclUint64, ncclSum, s.comm_nccl,
@@ -756,6 +808,8 @@ int reduce_u64(golhip_t h, const std::vector<unsigned long long *> &bufs, size_t
         if (i > 0)
             for (size_t j = 0; j < n; ++j) out[j] += tmp[j];
     }
+    if (h->host_comm_on && h->split && h->host_comm.allreduce_u64(h->host_comm.ctx, out, n) != 0)
+        return fail(h, GOLHIP_ERR_RCCL, "host transport: all-reduce of %zu counts failed", n);
     return GOLHIP_OK;
 }
 
@@ -837,18 +891,16 @@ int extract_cells(golhip_t h, const std::vector<const uint32_t *> &a,
     return sync_all(h);
 }
 
-// Host <-> device byte transfer of the handle's rows, in row chunks of <= 64 MiB staging.
+// Host <-> device byte transfer of the handle's rows, in row chunks through the shard's stage.
 int transfer_bytes(golhip_t h, uint8_t *host, size_t row_stride, bool to_device) {
     if (!host) return fail(h, GOLHIP_ERR_ARG, "buffer is null");
     if (row_stride < (size_t)h->width) return fail(h, GOLHIP_ERR_ARG, "row_stride < width");
     const int64_t W = h->width;
-    const int64_t chunk_rows = std::max<int64_t>(1, (64ll << 20) / W);
     int64_t hrow = 0;  // host row index relative to the handle's first row
     for (auto &s : h->shards) {
         HIPCHK(h, hipSetDevice(s.device));
-        uint8_t *stage = nullptr;
-        const int64_t cr = std::min(chunk_rows, s.rows);
-        HIPCHK(h, hipMalloc(&stage, (size_t)(cr * W)));
+        uint8_t *stage = s.stage;
+        const int64_t cr = std::min(std::max<int64_t>(1, s.stage_bytes / W), s.rows);
         for (int64_t y = 0; y < s.rows; y += cr) {
             const int64_t nr = std::min(cr, s.rows - y);
             uint32_t *rows_dev = h->row0(s, h->cur) + y * h->pitch;
@@ -865,7 +917,6 @@ int transfer_bytes(golhip_t h, uint8_t *host, size_t row_stride, bool to_device)
             }
             HIPCHK(h, hipStreamSynchronize(s.compute));
         }
-        HIPCHK(h, hipFree(stage));
         hrow += s.rows;
     }
     return GOLHIP_OK;
@@ -1132,6 +1183,51 @@ fail:
     return rc;
 }
 
+int golhip_create_rank_host(int width, int height, int rank, int world_size, int device, int k,
+                            const golhip_host_comm *comm, golhip_t *out) {
+    if (!out) return GOLHIP_ERR_ARG;
+    *out = nullptr;
+    if (!comm || !comm->exchange || !comm->allreduce_u64) return GOLHIP_ERR_ARG;
+    int rc = validate_geometry(width, height, world_size, k);
+    if (rc) return rc;
+    if (rank < 0 || rank >= world_size || device < 0) return GOLHIP_ERR_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) return GOLHIP_ERR_NODEV;
+    golhip_t h = new golhip_engine();
+    setup_engine(h, width, height, world_size, k);
+    h->rank_mode = true;
+    h->host_comm_on = true;
+    h->host_comm = *comm;
+    h->shards.resize(1);
+    Shard &s = h->shards[0];
+    s.device = device;
+    s.rank = rank;
+    strip_bounds(height, world_size, rank, s.y0, s.rows);
+    if ((rc = check_device_arch(h, device))) goto fail;
+    if ((rc = create_common(h))) goto fail;
+    if (h->split) {
+        (void)hipSetDevice(device);
+        const size_t bytes = (size_t)h->halo * (size_t)h->pitch * sizeof(uint32_t);
+        for (void *&b : h->hc_buf) {
+            const hipError_t e = hipHostMalloc(&b, bytes, hipHostMallocDefault);
+            if (e != hipSuccess) {
+                b = nullptr;
+                rc = fail(h, GOLHIP_ERR_OOM, "pinned halo buffers: %s", hipGetErrorString(e));
+                goto fail;
+            }
+        }
+    }
+    *out = h;
+    return GOLHIP_OK;
+fail:
+    g_create_error = h->err.empty() ? golhip_strerror(rc) : h->err;
+    for (auto &sh : h->shards) free_shard(sh);
+    for (void *b : h->hc_buf)
+        if (b) (void)hipHostFree(b);
+    delete h;
+    return rc;
+}
+
 int golhip_destroy(golhip_t h) {
     if (!h) return GOLHIP_ERR_ARG;
     for (auto &g : h->graphs) (void)hipGraphExecDestroy(g.exec);
@@ -1141,6 +1237,8 @@ int golhip_destroy(golhip_t h) {
         (void)hipEventDestroy(tp.b);
     }
     for (auto &s : h->shards) free_shard(s);
+    for (void *b : h->hc_buf)
+        if (b) (void)hipHostFree(b);
     delete h;
     return GOLHIP_OK;
 }
@@ -1207,14 +1305,16 @@ int golhip_store_words(golhip_t h, uint64_t *out) {
     int64_t hrow = 0;
     for (auto &s : h->shards) {
         HIPCHK(h, hipSetDevice(s.device));
-        uint64_t *d = nullptr;
-        HIPCHK(h, hipMalloc(&d, sizeof(uint64_t) * (size_t)(s.rows * wpr)));
-        HIPCHK(h, golhip::launch_words_out(h->row0(s, h->cur), h->pitch, s.rows, h->width, d,
-                                           s.compute));
-        HIPCHK(h, hipMemcpyAsync(out + hrow * wpr, d, sizeof(uint64_t) * (size_t)(s.rows * wpr),
-                                 hipMemcpyDeviceToHost, s.compute));
-        HIPCHK(h, hipStreamSynchronize(s.compute));
-        HIPCHK(h, hipFree(d));
+        uint64_t *d = reinterpret_cast<uint64_t *>(s.stage);
+        const int64_t cr = std::max<int64_t>(1, s.stage_bytes / (int64_t)sizeof(uint64_t) / wpr);
+        for (int64_t y = 0; y < s.rows; y += cr) {
+            const int64_t nr = std::min(cr, s.rows - y);
+            HIPCHK(h, golhip::launch_words_out(h->row0(s, h->cur) + y * h->pitch, h->pitch, nr,
+                                               h->width, d, s.compute));
+            HIPCHK(h, hipMemcpyAsync(out + (hrow + y) * wpr, d, sizeof(uint64_t) * (size_t)(nr * wpr),
+                                     hipMemcpyDeviceToHost, s.compute));
+            HIPCHK(h, hipStreamSynchronize(s.compute));
+        }
         hrow += s.rows;
     }
     return GOLHIP_OK;
@@ -1229,14 +1329,16 @@ int golhip_load_words(golhip_t h, const uint64_t *in) {
     int64_t hrow = 0;
     for (auto &s : h->shards) {
         HIPCHK(h, hipSetDevice(s.device));
-        uint64_t *d = nullptr;
-        HIPCHK(h, hipMalloc(&d, sizeof(uint64_t) * (size_t)(s.rows * wpr)));
-        HIPCHK(h, hipMemcpyAsync(d, in + hrow * wpr, sizeof(uint64_t) * (size_t)(s.rows * wpr),
-                                 hipMemcpyHostToDevice, s.compute));
-        HIPCHK(h, golhip::launch_words_in(d, s.rows, h->width, h->wd, h->row0(s, h->cur),
-                                          h->pitch, s.compute));
-        HIPCHK(h, hipStreamSynchronize(s.compute));
-        HIPCHK(h, hipFree(d));
+        uint64_t *d = reinterpret_cast<uint64_t *>(s.stage);
+        const int64_t cr = std::max<int64_t>(1, s.stage_bytes / (int64_t)sizeof(uint64_t) / wpr);
+        for (int64_t y = 0; y < s.rows; y += cr) {
+            const int64_t nr = std::min(cr, s.rows - y);
+            HIPCHK(h, hipMemcpyAsync(d, in + (hrow + y) * wpr, sizeof(uint64_t) * (size_t)(nr * wpr),
+                                     hipMemcpyHostToDevice, s.compute));
+            HIPCHK(h, golhip::launch_words_in(d, nr, h->width, h->wd, h->row0(s, h->cur) + y * h->pitch,
+                                              h->pitch, s.compute));
+            HIPCHK(h, hipStreamSynchronize(s.compute));
+        }
         hrow += s.rows;
     }
     h->turn = 0;
@@ -1251,6 +1353,10 @@ int golhip_load_words(golhip_t h, const uint64_t *in) {
 static int run_steps(golhip_t h, int64_t turns, uint64_t *alive_per_turn, bool ring) {
     if (!h || turns < 0) return GOLHIP_ERR_ARG;
     if (turns == 0) return GOLHIP_OK;
+    if ((ring || h->track_flips) && !variant_writes_flips(h->variant))
+        return fail(h, GOLHIP_ERR_STATE,
+                    "flips need a production kernel variant (GOLHIP_VARIANT=%d cannot write them)",
+                    h->variant);
     const bool counting = alive_per_turn != nullptr;
     if (counting) {
         for (auto &s : h->shards) {
@@ -1277,8 +1383,9 @@ static int run_steps(golhip_t h, int64_t turns, uint64_t *alive_per_turn, bool r
     const bool stream = !ring && h->shards.size() == 1 &&
                         pick_reg_kernel(h, h->shards[0].rows, kmax, counting).kind == 0 &&
                         pick_split(h, h->shards[0].rows, kmax) <= 1;
-    // planned per strip: the band geometry and each GPU's launch time follow the strip
-    LaunchPlanner plan((double)h->L * (double)h->shards[0].rows, ring ? 1 : h->k, turns,
+    // planned per strip (the band geometry and each GPU's launch time follow the strip), from the
+    // largest strip of the board, so every rank of a rank-mode board plans the same depths
+    LaunchPlanner plan((double)h->L * (double)plan_rows(h), ring ? 1 : h->k, turns,
                        !ring && graph_worthy(h, kmax), h->fixed_k || ring, h->track_flips,
                        h->count_window, stream);
     const int Kfull = plan.Kfull;
@@ -1353,9 +1460,11 @@ int golhip_step(golhip_t h, int64_t turns, uint64_t *alive_per_turn) {
 }
 
 // Ring slots per golhip_step_flips call: as many turns' flips boards as fit in ~1 GiB per strip
-// (5120^2: 319 turns; 512^2: 1024; 65536^2: 2).
+// (5120^2: 319 turns; 512^2: 1024; 65536^2: 2).  Every rank of a rank-mode board gets the same
+// capacity (that of the largest strip, plan_rows), so a call that fits on one rank fits on all and
+// no rank fails alone while the others block in the halo exchange.
 static int64_t ring_capacity(golhip_t h) {
-    int64_t rows = 1;
+    int64_t rows = std::max<int64_t>(1, plan_rows(h));
     for (auto &s : h->shards) rows = std::max(rows, s.rows);
     const int64_t board = rows * h->pitch * 4;
     return std::max<int64_t>(1, std::min<int64_t>(1024, ((int64_t)1 << 30) / board));
@@ -1409,6 +1518,10 @@ int golhip_flips_fetch(golhip_t h, int32_t *xy, size_t cap, size_t *n, uint64_t 
 
 int golhip_track_flips(golhip_t h, int enable) {
     if (!h) return GOLHIP_ERR_ARG;
+    if (enable && !variant_writes_flips(h->variant))
+        return fail(h, GOLHIP_ERR_STATE,
+                    "flips need a production kernel variant (GOLHIP_VARIANT=%d cannot write them)",
+                    h->variant);
     h->track_flips = enable != 0;
     if (h->track_flips)
         for (auto &s : h->shards)
@@ -1471,31 +1584,32 @@ static int ckpt_rows(golhip_t h, Shard &s, int64_t y, int64_t nr, uint8_t *host,
         HIPCHK(h, hipStreamSynchronize(s.compute));
         return GOLHIP_OK;
     }
-    std::vector<uint8_t> bytes((size_t)(nr * W));
-    uint8_t *stage = nullptr;
-    HIPCHK(h, hipMalloc(&stage, bytes.size()));
-    hipError_t e = hipSuccess;
-    if (to_device) {
-        for (int64_t r = 0; r < nr; ++r)
-            for (int64_t x = 0; x < W; ++x)
-                bytes[(size_t)(r * W + x)] = (host[r * rb + x / 8] >> (x % 8)) & 1 ? 255 : 0;
-        e = hipMemcpyAsync(stage, bytes.data(), bytes.size(), hipMemcpyHostToDevice, s.compute);
-        if (e == hipSuccess) e = golhip::launch_pack(stage, nr, W, h->wd, dev, h->pitch, s.compute);
-        if (e == hipSuccess) e = hipStreamSynchronize(s.compute);
-    } else {
-        e = golhip::launch_unpack(dev, h->pitch, nr, W, stage, s.compute);
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(bytes.data(), stage, bytes.size(), hipMemcpyDeviceToHost, s.compute);
-        if (e == hipSuccess) e = hipStreamSynchronize(s.compute);
-        if (e == hipSuccess) {
-            std::memset(host, 0, (size_t)(nr * rb));
-            for (int64_t r = 0; r < nr; ++r)
+    // the byte codec in row chunks through the shard's stage
+    const int64_t cr = std::max<int64_t>(1, s.stage_bytes / W);
+    std::vector<uint8_t> bytes((size_t)(std::min(cr, nr) * W));
+    uint8_t *stage = s.stage;
+    for (int64_t y0 = 0; y0 < nr; y0 += cr) {
+        const int64_t n = std::min(cr, nr - y0);
+        const size_t nb = (size_t)(n * W);
+        uint8_t *hrows = host + y0 * rb;
+        uint32_t *drows = dev + y0 * h->pitch;
+        if (to_device) {
+            for (int64_t r = 0; r < n; ++r)
                 for (int64_t x = 0; x < W; ++x)
-                    if (bytes[(size_t)(r * W + x)]) host[r * rb + x / 8] |= (uint8_t)(1u << (x % 8));
+                    bytes[(size_t)(r * W + x)] = (hrows[r * rb + x / 8] >> (x % 8)) & 1 ? 255 : 0;
+            HIPCHK(h, hipMemcpyAsync(stage, bytes.data(), nb, hipMemcpyHostToDevice, s.compute));
+            HIPCHK(h, golhip::launch_pack(stage, n, W, h->wd, drows, h->pitch, s.compute));
+            HIPCHK(h, hipStreamSynchronize(s.compute));
+        } else {
+            HIPCHK(h, golhip::launch_unpack(drows, h->pitch, n, W, stage, s.compute));
+            HIPCHK(h, hipMemcpyAsync(bytes.data(), stage, nb, hipMemcpyDeviceToHost, s.compute));
+            HIPCHK(h, hipStreamSynchronize(s.compute));
+            std::memset(hrows, 0, (size_t)(n * rb));
+            for (int64_t r = 0; r < n; ++r)
+                for (int64_t x = 0; x < W; ++x)
+                    if (bytes[(size_t)(r * W + x)]) hrows[r * rb + x / 8] |= (uint8_t)(1u << (x % 8));
         }
     }
-    (void)hipFree(stage);
-    HIPCHK(h, e);
     return GOLHIP_OK;
 }
 
@@ -1607,6 +1721,7 @@ int golhip_launch_plan(int64_t width, int64_t height, int strips, int k, int64_t
     if (width <= 0 || height <= 0 || strips <= 0 || k < 1 || k > golhip::kMaxK || turns < 0 || !n)
         return GOLHIP_ERR_ARG;
     const double cells = (double)lcm64(width, 128) * (double)height;
+    const double strip_cells = (double)lcm64(width, 128) * (double)strip_plan_rows(height, strips);
     const int Kfull = pick_k(k);
     // the engine's automatic choice for one strip: the register slab where the streaming kernel
     // would have at most 16 minimal-band waves per CU (256 CUs), else streaming (pick_reg_kernel)
@@ -1616,7 +1731,7 @@ int golhip_launch_plan(int64_t width, int64_t height, int strips, int k, int64_t
     const bool stream = strips > 1 || !golhip::stencil_slab_supported(Kfull, 8, Kfull == 16 ? 12 : 8,
                                                                        Kfull == 16 ? 2 : 4) ||
                         waves1 > 16 * 256;
-    LaunchPlanner plan(cells / strips, k, turns, strips == 1 && small_board(cells, Kfull), false, false,
+    LaunchPlanner plan(strip_cells, k, turns, strips == 1 && small_board(cells, Kfull), false, false,
                        4096, stream);
     size_t cnt = 0;
     while (plan.left > 0) {

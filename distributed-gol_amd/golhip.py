@@ -34,7 +34,8 @@ DENSITY_HALF = 0x80000000
 EXPORTS = [
     "golhip_version", "golhip_strerror", "golhip_device_count", "golhip_strip_bounds",
     "golhip_halo_plan",
-    "golhip_create", "golhip_create_strips", "golhip_nccl_unique_id", "golhip_create_rank", "golhip_destroy",
+    "golhip_create", "golhip_create_strips", "golhip_nccl_unique_id", "golhip_create_rank",
+    "golhip_create_rank_host", "golhip_destroy",
     "golhip_last_error", "golhip_get_info", "golhip_load_bytes", "golhip_init_random",
     "golhip_store_bytes", "golhip_store_words", "golhip_load_words", "golhip_step",
     "golhip_alive_count", "golhip_alive_cells", "golhip_flips", "golhip_turn",
@@ -54,6 +55,64 @@ class GolHipError(RuntimeError):
 class Xfer(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int32), ("peer", ctypes.c_int32), ("row", ctypes.c_int64),
                 ("nrows", ctypes.c_int64)]
+
+
+EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(Xfer), ctypes.c_int,
+                               ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                ctypes.c_size_t)
+
+
+class HostCommStruct(ctypes.Structure):
+    _fields_ = [("ctx", ctypes.c_void_p), ("exchange", EXCHANGE_FN), ("allreduce_u64", ALLREDUCE_FN)]
+
+
+class GlooHostComm:
+    """golhip_host_comm over a torch.distributed (gloo) process group: the halo exchange as
+    isend/irecv of the engine's pinned host buffers in the plan's order (gloo matches the i-th send
+    to a peer with that peer's i-th receive, as RCCL does inside a group), the count reduction as
+    one all_reduce.  The transport for ranks that cannot use RCCL peers (several ranks on one GPU
+    in the rank-mode tests: RCCL refuses a duplicate GPU)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+
+        self._dist, self._group = dist, group
+        self._exchange = EXCHANGE_FN(self._do_exchange)
+        self._allreduce = ALLREDUCE_FN(self._do_allreduce)
+        self.struct = HostCommStruct(None, self._exchange, self._allreduce)
+        self.exchanges = 0  # exchange calls seen (tests count them)
+        self.reduced = []   # sizes of the count reductions seen
+
+    def _do_exchange(self, _ctx, xfers, n, bufs, nbytes):
+        try:
+            reqs = []
+            for i in range(n):
+                x = xfers[i]
+                arr = np.ctypeslib.as_array(ctypes.cast(bufs[i], ctypes.POINTER(ctypes.c_uint8)),
+                                            shape=(nbytes,))
+                t = torch.from_numpy(arr)
+                op = self._dist.isend if x.kind == 0 else self._dist.irecv
+                reqs.append(op(t, x.peer, group=self._group))
+            for r in reqs:
+                r.wait()
+            self.exchanges += 1
+            return 0
+        except Exception as e:  # pragma: no cover - reported through the C ABI's error path
+            print(f"golhip host transport: exchange failed: {e!r}", flush=True)
+            return -1
+
+    def _do_allreduce(self, _ctx, vals, n):
+        try:
+            arr = np.ctypeslib.as_array(vals, shape=(n,)).view(np.int64)
+            t = torch.from_numpy(arr.copy())
+            self._dist.all_reduce(t, group=self._group)  # sum; uint64 wraps like int64
+            arr[:] = t.numpy()
+            self.reduced.append(int(n))
+            return 0
+        except Exception as e:  # pragma: no cover
+            print(f"golhip host transport: all_reduce failed: {e!r}", flush=True)
+            return -1
 
 
 class Info(ctypes.Structure):
@@ -91,6 +150,8 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
         "golhip_create_strips": ([i32, i32, i32, i32, i32, ctypes.POINTER(H)], i32),
         "golhip_nccl_unique_id": ([ctypes.c_char_p], i32),
         "golhip_create_rank": ([i32, i32, i32, i32, i32, i32, ctypes.c_char_p, ctypes.POINTER(H)], i32),
+        "golhip_create_rank_host": ([i32, i32, i32, i32, i32, i32, ctypes.POINTER(HostCommStruct),
+                                     ctypes.POINTER(H)], i32),
         "golhip_destroy": ([H], i32),
         "golhip_last_error": ([H], ctypes.c_char_p),
         "golhip_get_info": ([H, ctypes.POINTER(Info)], i32),
@@ -233,11 +294,15 @@ class Engine:
 
     def __init__(self, width: int, height: int, ngpus: int = 1, k: int = 1, *, rank: int | None = None,
                  world_size: int = 1, device: int = 0, nccl_id: bytes | None = None,
-                 strips: int | None = None):
+                 strips: int | None = None, host_comm: GlooHostComm | None = None):
         L = load_library()
         self._L = L
         self._h = ctypes.c_void_p()
-        if strips is not None:
+        self.host_comm = host_comm  # keeps the ctypes callbacks alive with the handle
+        if host_comm is not None:
+            rc = L.golhip_create_rank_host(width, height, rank or 0, world_size, device, k,
+                                           ctypes.byref(host_comm.struct), ctypes.byref(self._h))
+        elif strips is not None:
             rc = L.golhip_create_strips(width, height, strips, ngpus, k, ctypes.byref(self._h))
         elif rank is None:
             rc = L.golhip_create(width, height, ngpus, k, ctypes.byref(self._h))

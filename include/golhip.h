@@ -101,6 +101,24 @@ int golhip_create_strips(int width, int height, int nstrips, int ndevices, int k
 int golhip_nccl_unique_id(uint8_t *out /* GOLHIP_NCCL_ID_BYTES */);
 int golhip_create_rank(int width, int height, int rank, int world_size, int device, int k,
                        const uint8_t *nccl_id, golhip_t *out);
+/* The rank-mode engine with the caller's host transport in place of RCCL (the same strips,
+ * launch plan, halo plan, interior/boundary overlap and count reduction; only the transport
+ * differs).  Each K-block the engine copies its two send blocks of K rows to pinned host
+ * buffers and calls exchange() with the 4 transfers of golhip_halo_plan in issue order
+ * (bufs[i]: K * torus_width/8 bytes, a send's payload or a receive's destination; the i-th
+ * send to a peer must match that peer's i-th receive from this rank); allreduce_u64 sums n
+ * values over the ranks in place (per-turn counts, golhip_alive_count).  Both return 0 on
+ * success; anything else fails the call with GOLHIP_ERR_RCCL.  For hosts whose ranks cannot
+ * use RCCL peers -- e.g. several ranks sharing one GPU in a test, which RCCL refuses
+ * ("Duplicate GPU"); the cgo host would hand its own transport here the same way.  `comm` is
+ * copied; ctx must outlive the handle. */
+typedef struct {
+    void *ctx;
+    int (*exchange)(void *ctx, const golhip_xfer *xfers, int n, void *const *bufs, size_t bytes);
+    int (*allreduce_u64)(void *ctx, uint64_t *vals, size_t n);
+} golhip_host_comm;
+int golhip_create_rank_host(int width, int height, int rank, int world_size, int device, int k,
+                            const golhip_host_comm *comm, golhip_t *out);
 int golhip_destroy(golhip_t h);
 const char *golhip_last_error(golhip_t h);  /* h == NULL: why the last create failed (this thread) */
 int golhip_get_info(golhip_t h, golhip_info *out);
@@ -144,8 +162,11 @@ int golhip_step(golhip_t h, int64_t turns, uint64_t *alive_per_turn);
  * Broker.Publish, gol/distributor.go:48-49).  depths[i] > 0: one stencil launch of that many
  * generations; < 0: one captured graph replay of -depths[i] generations (small boards).  Large
  * boards run the depth <= k with the highest measured rate in bulk and split the last ones by a
- * modelled-time plan (e.g. 20 turns -> 10 + 10, not 16 + 4).  *n = number of entries; depths may
- * be NULL to size the array; GOLHIP_ERR_CAP if cap is too small. */
+ * modelled-time plan (e.g. 20 turns at 65536^2 -> 12 + 8, not 16 + 4).  Row strips are planned
+ * from the largest strip, ceil(height / strips) rows, so every rank of a rank-mode board runs this
+ * same sequence (each launch exchanges K-row halos) even when the strips differ by a row.
+ * *n = number of entries; depths may be NULL to size the array; GOLHIP_ERR_CAP if cap is too
+ * small. */
 int golhip_launch_plan(int64_t width, int64_t height, int strips, int k, int64_t turns,
                        int32_t *depths, size_t cap, size_t *n);
 /* Alive cells of the whole board (COLLECTIVE: sums over ranks). */

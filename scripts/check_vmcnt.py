@@ -19,8 +19,9 @@ For every such kernel in the given objects this script:
     of experimental variants (GOLHIP_VARIANT) and register-to-register spills (VGPR -> AGPR,
     SGPR -> VGPR lanes) are reported, not failed.
 
-Usage: check_vmcnt.py [--expect-fail] OBJ...   exit 0 = every kernel passes.  --expect-fail
-inverts that: exit 0 only if some kernel FAILS (the Makefile's self-test on guard_selftest.o, the
+Usage: check_vmcnt.py [--expect-fail | --scratch-only] OBJ...   exit 0 = every kernel passes.
+--scratch-only: only the scratch/spill check, on every kernel of the objects (register kernels).
+--expect-fail inverts the result: exit 0 only if some kernel FAILS (the Makefile's self-test on guard_selftest.o, the
 production K = 16 kernel forced to 8 waves per SIMD, which spills).
 """
 from __future__ import annotations
@@ -212,10 +213,36 @@ def check_object(obj: Path) -> tuple[int, list, list]:
     return checked, failures, notes
 
 
+def check_scratch_only(obj: Path) -> tuple[int, list, list]:
+    """Register kernels (gol_tile / gol_slab in stencil_tile.o: rows + chains held in VGPRs, no
+    LDS-DMA ring): every kernel must be scratch-free -- a spill there goes unnoticed otherwise."""
+    failures = []
+    with tempfile.TemporaryDirectory() as td:
+        co = device_object(obj, Path(td))
+        meta, code = kernel_metadata(co), kernel_code(co)
+    for name, ins in code.items():
+        md = meta.get(name, {})
+        errs = [f"{k} = {md[k]}" for k in ("private_segment_fixed_size", "vgpr_spill_count",
+                                            "sgpr_spill_count") if md.get(k, 0)]
+        if any(c[1].startswith("scratch_") for c in ins):
+            errs.append("scratch instructions present")
+        if errs:
+            failures.append((obj.name, name, errs))
+    return len(code), failures, []
+
+
 def main() -> int:
     args = sys.argv[1:]
     expect_fail = "--expect-fail" in args
     objs = [Path(a) for a in args if not a.startswith("--")]
+    if "--scratch-only" in args:
+        results = [check_scratch_only(o) for o in objs]
+        checked = sum(r[0] for r in results)
+        failures = [f for r in results for f in r[1]]
+        for obj, name, errs in failures:
+            print(f"FAIL {obj} {name}: {'; '.join(errs)}")
+        print(f"check_vmcnt --scratch-only: {checked} kernels checked, {len(failures)} use scratch")
+        return 1 if failures or checked == 0 else 0
     with ThreadPoolExecutor(max_workers=min(8, len(objs) or 1)) as pool:
         results = list(pool.map(check_object, objs))
     checked = sum(r[0] for r in results)

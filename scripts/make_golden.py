@@ -79,6 +79,41 @@ def cfg4():
                      "oracle_seconds": round(time.time() - t, 1)}}
 
 
+def weak():
+    """bench.py --gpus N (weak scaling): the 65536 x 65536*N board, random p=0.5 seed 3, split
+    into N row strips.  init_random numbers words over the WHOLE board, so the N-rank board is
+    this one global board.  Every per-turn count up to 1200 for N = 2, 4, 8 (the driver's run ends
+    at turn 5 + 20, the default one at 8 + 1000); N = 1 is cfg3_65536_seed3_counts.csv."""
+    out = {}
+    for n in (2, 4, 8):
+        w = oracle.init_random(65536, 65536 * n, seed=3)
+        t = time.time()
+        counts = oracle.packed_run_words(w, 1200, threads=8)
+        name = f"weak_65536x{65536 * n}_seed3_counts.csv"
+        write_counts_csv(name, counts)
+        out[f"weak{n}"] = {"width": 65536, "height": 65536 * n, "seed": 3, "csv_turns": 1200,
+                           "counts_csv": name, "digest_after_1200": oracle.digest_words(w),
+                           "oracle_seconds": round(time.time() - t, 1)}
+        del w
+        print("weak", n, out[f"weak{n}"]["oracle_seconds"], "s", flush=True)
+    return out
+
+
+def weak_small():
+    """Small weak-scaling boards for the rank-path tests (per-turn counts up to 1200, seed 3):
+    4096 x 4096*N (N = 2, 3; tests/test_bench_multirank_cpu.py) and 8192 x 8192*N (N = 2, 3;
+    bench.py --gpus N --size 8192 on one GPU with the host transport, tests/test_gpu_rank_host.py)."""
+    out = {}
+    for w, n in ((4096, 2), (4096, 3), (8192, 2), (8192, 3)):
+        b = oracle.init_random(w, w * n, seed=3)
+        counts = oracle.packed_run_words(b, 1200, threads=8)
+        name = f"weak_{w}x{w * n}_seed3_counts.csv"
+        write_counts_csv(name, counts)
+        out[f"weak_{w}x{w * n}"] = {"width": w, "height": w * n, "seed": 3, "csv_turns": 1200,
+                                     "counts_csv": name, "digest_after_1200": oracle.digest_words(b)}
+    return out
+
+
 def cfg5_board():
     import golhip
 

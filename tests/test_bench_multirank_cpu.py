@@ -1,20 +1,24 @@
-"""bench.py's N > 1 control flow on CPU: two gloo ranks run bench.main() exactly as
-`torch.distributed.run --nproc-per-node 2 bench.py --gpus 2 ...` would, with the GPU engine
-replaced by a host stand-in that records every step call.  The driver's 8-GPU scaling run is the
-only place the rank path meets hardware, so this checks what can break there without a GPU:
-every rank makes the same collective calls in the same order (barriers, the max-over-ranks
-timing, the pre-heat turn count taken from the cold pass), no N == 1-only leg runs, and rank 0
-prints one well-formed JSON line with the whole-job value.
+"""bench.py's N > 1 control flow on CPU: two and three gloo ranks run bench.main() exactly as
+`torch.distributed.run --nproc-per-node N bench.py --gpus N ...` would, with the GPU engine replaced
+by a host stand-in.  The driver's 8-GPU scaling run is the only place the RCCL rank path meets
+hardware, so this checks what can break there without a GPU: every rank makes the same collective
+calls in the same order (barriers, the max-over-ranks timing, the pre-heat turn count taken from
+the cold pass), no N == 1-only leg runs, rank 0 prints one well-formed JSON line with the whole-job
+value, and that line's `parity` is set and true: the N > 1 weak-scaling boards have committed
+oracle goldens (tests/golden/weak_*), and bench.py checks its alive count against them.
 
-The stand-in does no Life arithmetic (the GPU tests cover that); it sleeps in proportion to the
-cells a step updates so the timing path sees plausible numbers.
+The stand-in holds its own row strip (+ k halo rows each side) and really advances it: each
+k-block exchanges halos over gloo in golhip_halo_plan's order (the order the engine issues its
+RCCL send/recv in) and steps the halo'd strip with the CPU oracle; alive_count is the strip's
+popcount summed over the ranks (the engine's count all-reduce).  The GPU engine itself runs at
+world 2 and 3 in tests/test_gpu_rank_host.py (host transport instead of RCCL on one GPU).
 """
 import json
 import os
 import socket
 import sys
-import time
 
+import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
@@ -35,17 +39,21 @@ class _Info:
 
 
 class FakeEngine:
-    """Host stand-in for golhip.Engine in rank mode (the calls bench.py makes)."""
+    """Host stand-in for golhip.Engine in rank mode (the calls bench.py makes), stepping its strip
+    with the oracle and exchanging k-row halos with its ring neighbours over gloo."""
 
     log = []
 
     def __init__(self, width, height, ngpus=1, k=1, *, rank=None, world_size=None, device=0,
-                 nccl_id=None):
+                 nccl_id=None, host_comm=None):
         import golhip
 
         assert world_size and world_size > 1 and nccl_id is not None and len(nccl_id) > 0
-        y0, rows = golhip.strip_bounds(height, world_size, rank)
-        self.width, self.rows, self.k = width, rows, k
+        assert host_comm is None
+        self.y0, rows = golhip.strip_bounds(height, world_size, rank)
+        self.width, self.height, self.rows, self.k = width, height, rows, k
+        self.rank, self.world = rank, world_size
+        self.buf = np.zeros((rows + 2 * k, width // 64), dtype=np.uint64)
         self.info = _Info(rows)
         self.turn = 0
         self.timed = False
@@ -55,19 +63,61 @@ class FakeEngine:
         FakeEngine.log.append(("create", width, height, rank, world_size))
 
     def init_random(self, seed):
+        import oracle
+
+        k = self.k
+        self.buf[k:k + self.rows] = oracle.init_random(self.width, self.height, seed,
+                                                       y0=self.y0, y1=self.y0 + self.rows)
         self.turn = 0
         FakeEngine.log.append(("init", seed))
 
     def set_band_rows(self, n):
         pass
 
+    def _block(self, K):
+        import golhip
+        import oracle
+        import torch
+        import torch.distributed as dist
+
+        k, buf = self.k, self.buf
+        sent, recvd, reqs, landing = {}, {}, [], []
+        for kind, peer, row, n in golhip.halo_plan(self.height, self.world, self.rank, K):
+            if kind == "send":
+                tag = sent.get(peer, 0)
+                sent[peer] = tag + 1
+                t = torch.from_numpy(buf[k + row:k + row + n].view(np.int64).copy())
+                reqs.append(dist.isend(t, dst=peer, tag=tag))
+            else:
+                tag = recvd.get(peer, 0)
+                recvd[peer] = tag + 1
+                t = torch.empty((n, buf.shape[1]), dtype=torch.int64)
+                reqs.append(dist.irecv(t, src=peer, tag=tag))
+                landing.append((row, n, t))
+        for r in reqs:
+            r.wait()
+        for row, n, t in landing:
+            buf[k + row:k + row + n] = t.numpy().view(np.uint64)
+        # K generations of the strip with K halo rows each side: the rows past the halos are
+        # garbage that reaches the strip's own rows only after K generations
+        ext = np.ascontiguousarray(buf[k - K:k + self.rows + K])
+        oracle.packed_run_words(ext, K, threads=2)
+        buf[k:k + self.rows] = ext[K:K + self.rows]
+
     def step(self, turns, counts=False):
+        import time
+
         assert not counts
-        dt = self.width * self.rows * turns / 5e13  # ~50 TCUPS worth of sleeping
-        time.sleep(dt)
+        t0 = time.perf_counter()
+        left = turns
+        while left > 0:
+            K = min(self.k, left)
+            self._block(K)
+            left -= K
+            if self.timed:
+                self.launches += 1
         if self.timed:
-            self.t_ms += dt * 1e3
-            self.launches += -(-turns // self.k)
+            self.t_ms += (time.perf_counter() - t0) * 1e3
             self.gens += turns
         self.turn += turns
         FakeEngine.log.append(("step", turns))
@@ -85,7 +135,9 @@ class FakeEngine:
         import torch
         import torch.distributed as dist
 
-        t = torch.tensor([1000 + self.turn], dtype=torch.int64)  # collective, like the RCCL sum
+        own = self.buf[self.k:self.k + self.rows]
+        c = int(np.unpackbits(own.view(np.uint8)).sum())
+        t = torch.tensor([c], dtype=torch.int64)  # collective, like the engine's count all-reduce
         dist.all_reduce(t)
         return int(t.item())
 
@@ -150,3 +202,8 @@ def test_bench_rank_path_cpu(tmp_path, world):
     assert line["flips_path"] is None and line["cpu_baseline"] is None
     assert line["cold_start"]["preheat_turns"] >= 16
     assert line["strong_262144"]["rows_per_gpu"] == -(-2048 // world)
+    # the weak-scaling board (4096 x 4096*N, seed 3) is pinned: parity against the oracle golden
+    # at turn warmup + steps, in both the pre-heated and the cold-start pass
+    assert line["parity"] is not None and line["parity"]["turn"] == 25
+    assert line["parity"]["ok"] and line["parity"]["cold_start_ok"], line["parity"]
+    assert line["untimed_generations_before_value"] == 5 + 25 + line["cold_start"]["preheat_turns"]

@@ -128,3 +128,23 @@ def test_launch_plan_bulk_depth_by_board_size(golhip):
     assert graphs5k[:2] == [4096, 4096]  # the register slab keeps K = 16
     # the maximum depth still caps everything
     assert max(golhip.launch_plan(65536, 65536, 8, 1000)) <= 8
+
+
+@pytest.mark.parametrize("width,height,world", [(262144, 262143, 2), (65536, 65537, 2),
+                                                (4096, 4099, 4), (65536, 196607, 3)])
+def test_launch_plan_is_rank_independent_on_uneven_strips(golhip, width, height, world):
+    """Every launch of a split board exchanges K-row halos, so every rank of a rank-mode board must
+    run the same depths.  Strips differ by a row when height % world != 0; the planner ranks depths
+    from the largest strip, ceil(height / world) rows, which every rank shares (the engine's
+    run_steps and golhip_launch_plan use the same helper).  262143 rows on 2 ranks is the case
+    that split 131071 vs 131072 rows across the 2^35-cell bulk-depth switch (K = 12 vs 16)."""
+    rows = [golhip.strip_bounds(height, world, r)[1] for r in range(world)]
+    assert len(set(rows)) > 1  # the strips really are uneven
+    ceil_rows = -(-height // world)
+    for turns in (20, 25, 160, 1008):
+        plan = golhip.launch_plan(width, height, 16, turns, strips=world)
+        # the same plan as a board whose every strip has the largest strip's rows
+        assert plan == golhip.launch_plan(width, ceil_rows * world, 16, turns, strips=world)
+        assert sum(plan) == turns
+    if (width, height) == (262144, 262143):
+        assert set(golhip.launch_plan(width, height, 16, 160, strips=2)) == {16}

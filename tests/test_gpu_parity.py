@@ -486,3 +486,34 @@ def test_small_board_picks_register_slab(golhip, oracle):
     ref_counts = oracle.packed_run_words(words, 200)
     assert np.array_equal(got, words)
     assert np.array_equal(counts.astype(np.int64), ref_counts)
+
+
+@pytest.mark.parametrize("stage", [0, 4096])
+@pytest.mark.parametrize("shape", [(512, 512), (300, 1000), (96, 640)])
+def test_store_interleaved_with_steps(golhip, oracle, monkeypatch, tmp_path, stage, shape):
+    """The `s` snapshot path (gol/distributor.go:93-103,118-119): store_bytes / store_words /
+    checkpoint save+load between steps, through the shard's preallocated stage (no per-call device
+    allocation).  stage = 4096 shrinks the stage (GOLHIP_STAGE_BYTES) so every transfer runs in
+    many row chunks; each snapshot must equal the oracle at that turn."""
+    if stage:
+        monkeypatch.setenv("GOLHIP_STAGE_BYTES", str(stage))
+    h, w = shape
+    rng = np.random.default_rng(5)
+    board = np.where(rng.random((h, w)) < 0.4, 255, 0).astype(np.uint8)
+    ref = board.copy()
+    with golhip.Engine(w, h, k=16) as e:
+        e.load(board)
+        for i, n in enumerate([1, 16, 7, 33]):
+            e.step(n)
+            ref, _ = oracle.packed_run(ref, n)
+            assert np.array_equal(e.store(), ref), (i, n)
+            if w % 64 == 0:
+                assert np.array_equal(e.store_words(), oracle.pack(ref)[:, : w // 64])
+                e.load_words(oracle.pack(ref)[:, : w // 64])  # reload: the stage in the other way
+        e.checkpoint_save(str(tmp_path / "ckpt.bin"))
+        e.step(5)
+        e.checkpoint_load(str(tmp_path / "ckpt.bin"))
+        assert np.array_equal(e.store(), ref)
+        e.step(3)
+        ref, _ = oracle.packed_run(ref, 3)
+        assert np.array_equal(e.store(), ref)

@@ -1,0 +1,149 @@
+"""The rank-mode ENGINE at world 2 and 3 on one GPU: golhip_create_rank_host runs the same engine as
+golhip_create_rank -- per-rank strips, the rank-independent launch plan, golhip_halo_plan's transfer
+order, the interior launch overlapped with the two boundary bands, the per-turn count reduction --
+with the halos and count sums carried by a gloo host transport instead of RCCL (RCCL refuses two
+ranks on one device, and the test box has one GPU).  Every rank's strip, every per-turn count, the
+alive-cell list and the per-turn flips must equal the single-board oracle.
+
+Reference analogue: broker/broker.go:37-56 (strip fan-out), :168-174 (stitch),
+gol/distributor.go:53-59,153-166 (flips, alive cells); the reference broadcasts the whole world to
+every server instead of exchanging halos.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import PKG, ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+SCHEDULE = [1, 7, 20, 33, 16, 3]  # K = 1 launches, tail plans, bulk depths, a short call
+
+
+def _worker(rank, world, port, width, height, k, out_dir):
+    for p in (str(ROOT / "oracle"), str(PKG)):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    import golhip
+    import oracle
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = golhip.GlooHostComm()
+    res = {}
+    with golhip.Engine(width, height, k=k, rank=rank, world_size=world, device=0,
+                       host_comm=comm) as e:
+        y0, rows = e.info.y0, e.info.rows
+        assert (y0, rows) == golhip.strip_bounds(height, world, rank)
+        e.load_words(oracle.init_random(width, height, seed=11)[y0:y0 + rows])
+        counts = [e.step(n, counts=True) for n in SCHEDULE]
+        res["counts"] = np.concatenate(counts)
+        res["alive"] = np.array([e.alive_count()])
+        res["words"] = e.store_words()
+        res["cells"] = e.alive_cells()
+        # fixed-depth launches (every launch exactly 4 deep, then a 2-deep tail)
+        e.set_fixed_k(True)
+        e.set_k(4)
+        res["counts_fixed"] = e.step(10, counts=True)
+        e.set_fixed_k(False)
+        e.set_k(k)
+        # per-turn flips ring (one K = 1 launch and one exchange per turn)
+        per_turn, alive = e.step_flips(5, counts=True)
+        res["flips_n"] = np.array([len(x) for x in per_turn])
+        res["flips"] = np.concatenate([x for x in per_turn]) if any(len(x) for x in per_turn) \
+            else np.zeros((0, 2), np.int32)
+        res["flips_alive"] = alive
+        res["words_end"] = e.store_words()
+    res["exchanges"] = np.array([comm.exchanges])
+    res["reduced"] = np.array(comm.reduced)
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,width,height,k", [
+    (2, 1024, 1001, 16),   # uneven strips (500 / 501 rows)
+    (3, 1024, 1000, 16),   # 333 / 333 / 334
+    (2, 2048, 40, 16),     # strips shorter than 3k: the boundary launch waits for the halos
+    (3, 576, 197, 8),      # width not a multiple of 128 (the torus is replicated horizontally)
+])
+def test_rank_engine_host_transport_matches_oracle(tmp_path, oracle, world, width, height, k):
+    mp.start_processes(_worker, args=(world, _free_port(), width, height, k, str(tmp_path)),
+                       nprocs=world, join=True, start_method="spawn")
+    r = [dict(np.load(tmp_path / f"rank{i}.npz")) for i in range(world)]
+    ref = oracle.init_random(width, height, seed=11)
+    turns = sum(SCHEDULE)
+    exp_counts = oracle.packed_run_words(ref, turns)
+    for i in range(world):  # the count reduction hands every rank the whole board's counts
+        assert np.array_equal(r[i]["counts"].astype(np.int64), exp_counts), i
+        assert int(r[i]["alive"][0]) == int(exp_counts[-1])
+    assert np.array_equal(np.concatenate([x["words"] for x in r]), ref)
+    # alive cells: each rank lists its own strip's cells (global y), row-major
+    cells = np.concatenate([x["cells"] for x in r])
+    ys, xs = np.nonzero(oracle.unpack(ref, width) == 255)
+    assert np.array_equal(cells, np.stack([xs, ys], axis=1).astype(np.int32))
+    exp_fixed = oracle.packed_run_words(ref, 10)
+    for i in range(world):
+        assert np.array_equal(r[i]["counts_fixed"].astype(np.int64), exp_fixed)
+    # per-turn flips: per rank its strip's flips of each turn; together the board's
+    prev = oracle.unpack(ref, width)
+    off = [0] * world
+    for t in range(5):
+        c = oracle.packed_run_words(ref, 1)
+        cur = oracle.unpack(ref, width)
+        ys, xs = np.nonzero(prev != cur)
+        want = np.stack([xs, ys], axis=1).astype(np.int32)
+        got = []
+        for i in range(world):
+            n = int(r[i]["flips_n"][t])
+            got.append(r[i]["flips"][off[i]:off[i] + n])
+            off[i] += n
+            assert int(r[i]["flips_alive"][t]) == int(c[0])
+        assert np.array_equal(np.concatenate(got), want), t
+        prev = cur
+    assert np.array_equal(np.concatenate([x["words_end"] for x in r]), ref)
+    # the transport really carried the exchanges: one per launch; count sums of every call
+    ex = [int(x["exchanges"][0]) for x in r]
+    assert len(set(ex)) == 1 and ex[0] >= len(SCHEDULE) + 5
+    assert all(np.array_equal(x["reduced"], r[0]["reduced"]) for x in r)
+
+
+@pytest.mark.timeout(700)
+def test_bench_rank_path_host_transport(tmp_path):
+    """bench.py --gpus 2 and 3 as torch.distributed.run launches it, the ranks sharing this GPU
+    through the host transport (GOLHIP_HOST_COMM=1): the real engine, launch plan and timed region
+    at N > 1; the line's parity (8192 x 8192*N board, seed 3, oracle golden CSV) must hold."""
+    for world in (2, 3):
+        env = dict(os.environ, GOLHIP_HOST_COMM="1", PYTHONUNBUFFERED="1")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={world}", "--master-addr", "127.0.0.1",
+               "--master-port", str(_free_port()), str(ROOT / "bench.py"), "--gpus", str(world),
+               "--size", "8192", "--steps", "40", "--warmup", "5", "--no-strong",
+               "--preheat-ms", "20"]
+        p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+        lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+        assert len(lines) == 1, p.stdout
+        line = json.loads(lines[0])
+        (tmp_path / f"bench_world{world}.json").write_text(lines[0])
+        assert line["n_gpus"] == world and line["config"]["height"] == 8192 * world
+        assert line["parity"] is not None and line["parity"]["ok"], line["parity"]
+        assert line["parity"]["cold_start_ok"]
+        assert line["transport"].startswith("gloo host transport")
