@@ -61,6 +61,7 @@ struct Shard {
     uint32_t *ex_rowcounts = nullptr;
     unsigned long long *ex_offsets = nullptr;
     unsigned long long *ex_slot_counts = nullptr;
+    unsigned long long *ex_block_sums = nullptr;  // kScanBlocks: the multi-block scan's partials
     int64_t ex_rows_cap = 0, ex_slots_cap = 0;
     int32_t *ex_xy = nullptr;
     size_t ex_xy_cap = 0;
@@ -188,6 +189,8 @@ int ensure_extract_scratch(golhip_t h, Shard &s, int64_t rows, int64_t slots) {
     if (rows <= s.ex_rows_cap && slots <= s.ex_slots_cap) return GOLHIP_OK;
     HIPCHK(h, hipSetDevice(s.device));
     HIPCHK(h, hipStreamSynchronize(s.compute));
+    if (!s.ex_block_sums)
+        HIPCHK(h, hipMalloc(&s.ex_block_sums, sizeof(unsigned long long) * golhip::kScanBlocks));
     if (rows > s.ex_rows_cap) {
         if (s.ex_rowcounts) HIPCHK(h, hipFree(s.ex_rowcounts));
         if (s.ex_offsets) HIPCHK(h, hipFree(s.ex_offsets));
@@ -249,7 +252,8 @@ void free_shard(Shard &s) {
     if (s.scratch_u64) (void)hipFree(s.scratch_u64);
     if (s.d_counts) (void)hipFree(s.d_counts);
     for (void *q : {(void *)s.diffbuf, (void *)s.ring, (void *)s.ex_rowcounts, (void *)s.ex_offsets,
-                    (void *)s.ex_slot_counts, (void *)s.ex_xy, (void *)s.stage})
+                    (void *)s.ex_slot_counts, (void *)s.ex_xy, (void *)s.stage,
+                    (void *)s.ex_block_sums})
         if (q) (void)hipFree(q);
     if (s.ev_ready) (void)hipEventDestroy(s.ev_ready);
     if (s.ev_halo) (void)hipEventDestroy(s.ev_halo);
@@ -735,6 +739,9 @@ int step_block(golhip_t h, int K, int64_t slot_gen, int64_t diff_slot = kDiffNon
         if (!h->split) {
             StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0);
             p.diff = diff;
+            // a K-deep ring launch (ring_depth: a production register slab) writes the flips of
+            // each of its K generations into K consecutive ring slots
+            p.diff_stride = diff_slot >= 0 && K > 1 ? s.rows * h->pitch : 0;
             HIPCHK(h, launch_auto(h, K, in, out, p, slots, s.compute));
         } else if (s.rows >= 3 * K) {
             // The interior rows need no halo: they run while the halos are exchanged.  The two
@@ -766,6 +773,21 @@ int step_block(golhip_t h, int K, int64_t slot_gen, int64_t diff_slot = kDiffNon
     h->prev_valid = (K == 1);
     h->diff_valid = diff_slot == kDiffLast;
     return GOLHIP_OK;
+}
+
+// Depth of the next launch of golhip_step_flips (`left` turns to go): a register-slab launch of K
+// generations writes K consecutive ring slots (every generation's flips, gol_slab LD = 2), so the
+// ring runs the deepest depth <= left for which the board's automatic kernel choice is a
+// production slab shape; anything else (strips, the streaming kernel of large boards, the tail)
+// runs one-generation launches, each writing its slot.
+int ring_depth(golhip_t h, int64_t left, bool counting) {
+    if (h->split || h->shards.size() != 1) return 1;
+    for (int K : {16, 12, 8}) {
+        if (K > left || K > h->k) continue;
+        const RegKernel rk = pick_reg_kernel(h, h->shards[0].rows, K, counting);
+        if (rk.kind == 3 && golhip::stencil_slab_flips_every_gen(K, rk.W, rk.S, rk.NC)) return K;
+    }
+    return 1;
 }
 
 // Per-generation counts of the first n window generations -> s.d_counts[off, off + n), one
@@ -831,7 +853,8 @@ int extract_cells(golhip_t h, const std::vector<const uint32_t *> &a,
         if (rc) return rc;
         HIPCHK(h, hipSetDevice(s.device));
         HIPCHK(h, golhip::launch_extract_count(a[i], b[i], h->pitch, rows, h->width,
-                                               s.ex_rowcounts, s.ex_offsets, s.compute));
+                                               s.ex_rowcounts, s.ex_offsets, s.ex_block_sums,
+                                               s.compute));
         HIPCHK(h, golhip::launch_extract_slot_counts(s.ex_offsets, s.rows, slots, s.ex_slot_counts,
                                                      s.compute));
         HIPCHK(h, hipMemcpyAsync(cnt[i].data(), s.ex_slot_counts,
@@ -877,6 +900,12 @@ int extract_cells(golhip_t h, const std::vector<const uint32_t *> &a,
                                               s.ex_offsets, s.y0, s.rows, s.ex_xy,
                                               shard_total[i], s.compute));
         // the shard's list is slot-major; copy each slot's run to its place in the global list
+        // (one shard: the shard's list IS the global list, one copy)
+        if (ns == 1) {
+            HIPCHK(h, hipMemcpyAsync(xy, s.ex_xy, sizeof(int32_t) * 2 * shard_total[i],
+                                     hipMemcpyDeviceToHost, s.compute));
+            continue;
+        }
         size_t src = 0;
         for (int64_t t = 0; t < slots; ++t) {
             size_t dst = slot_base[t];
@@ -1391,7 +1420,7 @@ static int run_steps(golhip_t h, int64_t turns, uint64_t *alive_per_turn, bool r
     const int Kfull = plan.Kfull;
     int64_t win = 0;  // generations pending in the count window, from turn offset done - win
     while (done < turns) {
-        const int K = plan.next();
+        const int K = ring ? ring_depth(h, turns - done, counting) : plan.next();
         if (K == 0) {  // one graph replay of M x Kfull generations
             const int M = plan.last_M;
             if (counting) {  // the graph finalizes its own generations from window slot 0

@@ -31,6 +31,9 @@ struct StencilParams {
     // generation with the one before it -- the cells the launch's last generation flipped
     // (gol/distributor.go:53-59), written beside the output rows (no extra pass)
     uint32_t *diff;
+    // > 0 (gol_slab only; golhip_step_flips): EVERY generation g (0-based) of the launch writes its
+    // flips to diff + g * diff_stride words (consecutive slots of the per-turn flips ring)
+    int64_t diff_stride;
 };
 
 constexpr int kMaxK = 32;         // generations per launch limit (halo lane = 32 bits)
@@ -126,6 +129,9 @@ hipError_t launch_stencil_slab(int K, int W, int S, int NC, const uint32_t *in_r
                                const StencilParams &p, unsigned long long *count_slots,
                                hipStream_t s);
 bool stencil_slab_supported(int K, int W, int S, int NC = 4);
+// the slab shapes that can write EVERY generation's flips (StencilParams::diff_stride > 0): the
+// production shapes pick_reg_kernel chooses
+bool stencil_slab_flips_every_gen(int K, int W, int S, int NC = 4);
 hipError_t warm_stencil_tile(hipStream_t s);
 constexpr int kTileChunkWords = 62;
 // Words per column chunk of the level-split kernel (half-word halo for K <= 16).
@@ -150,10 +156,15 @@ hipError_t launch_init_random(uint32_t *row0, int64_t pitch, int64_t rows, int64
 hipError_t launch_popcount(const uint32_t *row0, int64_t pitch, int64_t rows, int32_t wd,
                            unsigned long long *out, hipStream_t s);
 // Alive-cell / flip extraction (row-major): cells are bits of (a ^ b) (b nullable) in the first
-// `width` columns.  row_counts[rows], offsets[rows+1] are scratch; offsets[rows] = total.
+// `width` columns.  row_counts[rows], offsets[rows+1], block_sums[kScanBlocks] are scratch;
+// offsets = the exclusive scan of the row counts, offsets[rows] = total.  Multi-block: every
+// block counts a contiguous range of rows, one block scans the block sums, every block then scans
+// its range (three launches, no serial walk over the rows).
+constexpr int kScanBlocks = 1024;
 hipError_t launch_extract_count(const uint32_t *a, const uint32_t *b, int64_t pitch,
                                 int64_t rows, int64_t width, uint32_t *row_counts,
-                                unsigned long long *offsets, hipStream_t s);
+                                unsigned long long *offsets, unsigned long long *block_sums,
+                                hipStream_t s);
 // slot_rows: rows per slot of a tall board of slots (y is reported within its slot).
 hipError_t launch_extract_emit(const uint32_t *a, const uint32_t *b, int64_t pitch,
                                int64_t rows, int64_t width, const unsigned long long *offsets,

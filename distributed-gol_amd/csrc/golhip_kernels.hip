@@ -159,44 +159,83 @@ __device__ __forceinline__ uint32_t cell_word(const uint32_t *a, const uint32_t 
     return v;
 }
 
+// Phase 1: block b counts rows [b * per, (b + 1) * per) (one wave per row at a time) into
+// row_counts and their total into block_sums[b].
 __global__ void extract_count(const uint32_t *__restrict__ a, const uint32_t *__restrict__ b,
-                              int64_t pitch, int64_t rows, int32_t nw, uint32_t lastmask,
-                              uint32_t *__restrict__ row_counts) {
-    const int lane = threadIdx.x & 63;
-    const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
-    for (int64_t y = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); y < rows;
-         y += nwaves) {
+                              int64_t pitch, int64_t rows, int64_t per, int32_t nw,
+                              uint32_t lastmask, uint32_t *__restrict__ row_counts,
+                              unsigned long long *__restrict__ block_sums) {
+    __shared__ unsigned long long part[4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t y0 = (int64_t)blockIdx.x * per, y1 = min(rows, y0 + per);
+    unsigned long long tot = 0;
+    for (int64_t y = y0 + wv; y < y1; y += 4) {
         uint32_t c = 0;
         for (int32_t col = lane; col < nw; col += 64)
             c += __builtin_popcount(cell_word(a, b, y * pitch + col, col, nw, lastmask));
         c = wave_sum_u32(c);
         if (lane == 0) row_counts[y] = c;
+        tot += c;
     }
+    if (lane == 0) part[wv] = tot;
+    __syncthreads();
+    if (threadIdx.x == 0) block_sums[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
 }
 
-__global__ void extract_scan(const uint32_t *__restrict__ row_counts, int64_t rows,
-                             unsigned long long *__restrict__ offsets) {
-    __shared__ unsigned long long part[1024];
-    const int t = threadIdx.x, nt = blockDim.x;
-    const int64_t per = (rows + nt - 1) / nt, b0 = t * per, b1 = min(rows, b0 + per);
-    unsigned long long s = 0;
-    for (int64_t i = b0; i < b1; ++i) s += row_counts[i];
-    part[t] = s;
-    __syncthreads();
-    if (t == 0) {
-        unsigned long long run = 0;
-        for (int i = 0; i < nt; ++i) {
-            const unsigned long long x = part[i];
-            part[i] = run;
-            run += x;
-        }
-        offsets[rows] = run;
+// Inclusive scan of one value per thread over a 256-thread block (4 waves, shuffles + LDS).
+__device__ __forceinline__ unsigned long long block_scan_incl(unsigned long long v,
+                                                               unsigned long long *wsum) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const unsigned long long t = __shfl_up(v, off, 64);
+        if (lane >= off) v += t;
     }
+    if (lane == 63) wsum[wv] = v;
     __syncthreads();
-    unsigned long long run = part[t];
-    for (int64_t i = b0; i < b1; ++i) {
-        offsets[i] = run;
-        run += row_counts[i];
+    unsigned long long add = 0;
+    for (int w = 0; w < wv; ++w) add += wsum[w];
+    __syncthreads();
+    return v + add;
+}
+
+// Phase 2 (one block of kScanBlocks threads): block_sums -> their exclusive scan, in place;
+// offsets[rows] = the total.
+__global__ void extract_scan_blocks(unsigned long long *__restrict__ block_sums, int nb,
+                                    unsigned long long *__restrict__ total) {
+    __shared__ unsigned long long wsum[16];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    unsigned long long v = t < nb ? block_sums[t] : 0ull, x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const unsigned long long u = __shfl_up(x, off, 64);
+        if (lane >= off) x += u;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    unsigned long long add = 0;
+    for (int w = 0; w < wv; ++w) add += wsum[w];
+    if (t < nb) block_sums[t] = add + x - v;
+    if (t == (int)blockDim.x - 1) *total = add + x;
+}
+
+// Phase 3: block b writes the exclusive offsets of its rows (tiles of 256 rows, block scans).
+__global__ void extract_scan_rows(const uint32_t *__restrict__ row_counts, int64_t rows, int64_t per,
+                                  const unsigned long long *__restrict__ block_offs,
+                                  unsigned long long *__restrict__ offsets) {
+    __shared__ unsigned long long wsum[4];
+    __shared__ unsigned long long carry;
+    const int64_t y0 = (int64_t)blockIdx.x * per, y1 = min(rows, y0 + per);
+    unsigned long long run = block_offs[blockIdx.x];
+    for (int64_t t0 = y0; t0 < y1; t0 += 256) {
+        const int64_t y = t0 + threadIdx.x;
+        const unsigned long long v = y < y1 ? row_counts[y] : 0ull;
+        const unsigned long long incl = block_scan_incl(v, wsum);
+        if (y < y1) offsets[y] = run + incl - v;
+        if (threadIdx.x == 255) carry = incl;
+        __syncthreads();
+        run += carry;
+        __syncthreads();
     }
 }
 
@@ -370,16 +409,24 @@ static void extract_geometry(int64_t width, int32_t &nw, uint32_t &lastmask) {
 
 hipError_t launch_extract_count(const uint32_t *a, const uint32_t *b, int64_t pitch,
                                 int64_t rows, int64_t width, uint32_t *row_counts,
-                                unsigned long long *offsets, hipStream_t s) {
+                                unsigned long long *offsets, unsigned long long *block_sums,
+                                hipStream_t s) {
     int32_t nw;
     uint32_t lastmask;
     extract_geometry(width, nw, lastmask);
-    const unsigned blocks = grid_for(rows * 64, 256, 16384);
-    hipLaunchKernelGGL(extract_count, dim3(blocks), dim3(256), 0, s, a, b, pitch, rows, nw,
-                       lastmask, row_counts);
+    // contiguous row ranges of >= 16 rows per block, at most kScanBlocks blocks
+    const int64_t per = std::max<int64_t>(16, (rows + kScanBlocks - 1) / kScanBlocks);
+    const int nb = (int)std::max<int64_t>(1, (rows + per - 1) / per);
+    hipLaunchKernelGGL(extract_count, dim3(nb), dim3(256), 0, s, a, b, pitch, rows, per, nw,
+                       lastmask, row_counts, block_sums);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(extract_scan, dim3(1), dim3(1024), 0, s, row_counts, rows, offsets);
+    hipLaunchKernelGGL(extract_scan_blocks, dim3(1), dim3(kScanBlocks), 0, s, block_sums, nb,
+                       offsets + rows);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(extract_scan_rows, dim3(nb), dim3(256), 0, s, row_counts, rows, per,
+                       block_sums, offsets);
     return hipGetLastError();
 }
 

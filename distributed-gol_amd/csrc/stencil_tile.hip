@@ -279,13 +279,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) voi
     }
 }
 
+// A drifted row of generation g (0-based; g + 1 bits east of the board frame) moved back, for
+// runtime g: the lane's word takes its upper 31 - g bits and the east lane's low g + 1 bits.
+__device__ __forceinline__ uint32_t realign_drift_rt(uint32_t v, int g) {
+    return __builtin_amdgcn_alignbit(lane_from_east(v), v, (uint32_t)(g + 1));
+}
+
 // gol_slab: the register tile spread over the W waves of a workgroup.  Wave w holds S rows of the
 // slab's W*S (a 62-word column chunk, rows ya - K + wS ...) in c[1..S]; each generation the waves
 // swap their edge rows through LDS (c[0] = the row above, c[S+1] = the row below, double-buffered
 // by generation parity: one barrier per generation) and update their S rows.  The trapezoid is
 // paid once per slab (2K rows of W*S) instead of once per wave, with S-row waves: more waves per
 // SIMD at the same work.  Output: the T = W*S - 2K middle rows.
-template <int K, int W, int S, bool COUNT, bool LD, int NC = kTileChains>
+// LD: 0 no flips, 1 the last generation's flips to p.diff, 2 EVERY generation's flips to
+// p.diff + g * p.diff_stride (golhip_step_flips: one K-deep launch fills K slots of the per-turn
+// flips ring; the output rows are valid at every generation of the trapezoid, and each
+// generation's new row and the centre cells it replaces sit in the same drifted frame).
+template <int K, int W, int S, bool COUNT, int LD, int NC = kTileChains>
 __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ in,
                                                    uint32_t *__restrict__ out, StencilParams p,
                                                    unsigned long long *__restrict__ slots) {
@@ -323,7 +333,7 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
     const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
         out + (int64_t)ya * p.pitch, 0, nrows * rowbytes, kBufferRsrcWord3);
     __amdgpu_buffer_rsrc_t drsrc = orsrc;
-    if constexpr (LD)
+    if constexpr (LD == 1)
         drsrc = __builtin_amdgcn_make_buffer_rsrc(p.diff + (int64_t)ya * p.pitch, 0,
                                                   nrows * rowbytes, kBufferRsrcWord3);
     const LaneStore ls = lane_store<false>(lane, colraw, col, p.wd);
@@ -373,6 +383,10 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
         constexpr bool LAST = decltype(last_c)::value, FULL = decltype(full_c)::value;
         constexpr bool CNT = COUNT && decltype(cnt_c)::value;
         uint32_t cnt = 0;
+        __amdgpu_buffer_rsrc_t grsrc = orsrc;  // LD == 2: this generation's flips ring slot
+        if constexpr (LD == 2)
+            grsrc = __builtin_amdgcn_make_buffer_rsrc(p.diff + gen * p.diff_stride + (int64_t)ya * p.pitch,
+                                                      0, nrows * rowbytes, kBufferRsrcWord3);
         // (segment 0 bottom-up, REV0 -- the hand-off row above needed only at its last step --
         // measured 3-7 % slower: profiles/r02/small_boards.txt)
         gen_rows<1, S, !LAST, NC>(c, [&](auto rc, uint32_t nx, uint32_t centre) {
@@ -380,12 +394,17 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
             const int o = o0 + r - 1;
             const bool mine = FULL || (o >= 0 && o < nrows);  // wave-uniform
             if (CNT) cnt += __builtin_popcount(mine ? nx : 0u);
+            if constexpr (LD == 2) {  // every generation's flips (output rows only)
+                Words<1> dv;
+                dv.w[0] = realign_drift_rt(nx ^ centre, gen);
+                golhip::store_row<1, false>(grsrc, ls, dv, mine ? o * rowbytes : kOutOfRange);
+            }
             if constexpr (LAST) {
                 const int rowoff = mine ? o * rowbytes : kOutOfRange;
                 Words<1> v;
                 v.w[0] = realign_drift<K>(nx);
                 golhip::store_row<1, false>(orsrc, ls, v, rowoff);
-                if constexpr (LD) {
+                if constexpr (LD == 1) {
                     Words<1> dv;
                     dv.w[0] = realign_drift<K>(nx ^ centre);
                     golhip::store_row<1, false>(drsrc, ls, dv, rowoff);
@@ -401,7 +420,25 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
     // variants inside the loop makes the allocator reconcile c[] with v_movs every generation).
     // Slab rows [w*S, w*S + S) of this wave; generation g is valid on [g, W*S - g), so from
     // generation g_end = min(w*S + S, W*S - w*S) on all of a wave's rows are outside it.
-    if constexpr (!COUNT) {
+    if constexpr (LD == 2) {
+        // every generation's flips: halo waves run their dead generations too (they store
+        // nothing: no output rows), so every wave runs one loop of one pass body
+        if (full) {
+#pragma clang loop unroll(disable)
+            for (int g = 1; g < K; ++g) {
+                exchange(g);
+                pass(No{}, Yes{}, Yes{}, g - 1);
+            }
+        } else {
+#pragma clang loop unroll(disable)
+            for (int g = 1; g < K; ++g) {
+                exchange(g);
+                pass(No{}, No{}, Yes{}, g - 1);
+            }
+        }
+        exchange(K);
+        pass(Yes{}, No{}, Yes{}, K - 1);
+    } else if constexpr (!COUNT) {
         // without counts every wave runs every generation: measured faster than skipping the
         // halo waves' dead generations (0.815 vs 0.847 us/turn at 5120^2, profiles/r02/r02z_slab_ab.txt)
 #pragma clang loop unroll(disable)
@@ -472,21 +509,39 @@ hipError_t launch_tile_kt(const uint32_t *in, uint32_t *out, const StencilParams
     return hipGetLastError();
 }
 
+// The production slab shapes (pick_reg_kernel): only these instantiate the every-generation
+// flips variant (LD = 2).
+constexpr bool slab_prod_shape(int K, int W, int S, int NC) {
+    return (K == 16 && W == 8 && S == 12 && NC == 2) || (K == 16 && W == 12 && S == 8 && NC == 2) ||
+           (K == 8 && W == 8 && S == 8 && NC == 4) || (K == 12 && W == 8 && S == 8 && NC == 4);
+}
+
 template <int K, int W, int S, int NC>
 hipError_t launch_slab_kws(const uint32_t *in, uint32_t *out, const StencilParams &p,
                            unsigned long long *slots, hipStream_t s) {
     const int64_t ngroups = p.nbands * (int64_t)p.nchunks;
     const unsigned blocks = (unsigned)std::max<int64_t>(1, (ngroups + kXcds - 1) / kXcds * kXcds);
     const dim3 block(64 * W);
+    if (p.diff && p.diff_stride > 0) {
+        if constexpr (slab_prod_shape(K, W, S, NC)) {
+            if (slots)
+                hipLaunchKernelGGL((gol_slab<K, W, S, true, 2, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
+            else
+                hipLaunchKernelGGL((gol_slab<K, W, S, false, 2, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
+            return hipGetLastError();
+        } else {
+            return hipErrorNotSupported;
+        }
+    }
     if (p.diff) {
         if (slots)
-            hipLaunchKernelGGL((gol_slab<K, W, S, true, true, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
+            hipLaunchKernelGGL((gol_slab<K, W, S, true, 1, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
         else
-            hipLaunchKernelGGL((gol_slab<K, W, S, false, true, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
+            hipLaunchKernelGGL((gol_slab<K, W, S, false, 1, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
     } else if (slots) {
-        hipLaunchKernelGGL((gol_slab<K, W, S, true, false, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
+        hipLaunchKernelGGL((gol_slab<K, W, S, true, 0, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
     } else {
-        hipLaunchKernelGGL((gol_slab<K, W, S, false, false, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
+        hipLaunchKernelGGL((gol_slab<K, W, S, false, 0, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
     }
     return hipGetLastError();
 }
@@ -500,6 +555,10 @@ hipError_t launch_slab_kws(const uint32_t *in, uint32_t *out, const StencilParam
     X(16, 8, 14, 4) X(16, 8, 16, 4) X(16, 8, 20, 4) X(16, 8, 24, 4) X(16, 16, 4, 4) X(16, 16, 6, 4) \
     X(16, 16, 8, 4) X(16, 16, 16, 4) X(16, 4, 16, 4) X(16, 4, 24, 4) X(16, 8, 12, 2) X(16, 8, 12, 3) \
     X(16, 12, 8, 2) X(16, 12, 8, 4)
+
+bool stencil_slab_flips_every_gen(int K, int W, int S, int NC) {
+    return stencil_slab_supported(K, W, S, NC) && slab_prod_shape(K, W, S, NC);
+}
 
 bool stencil_slab_supported(int K, int W, int S, int NC) {
 #define GOLHIP_X(KK, WW, SS, NN) \
@@ -545,7 +604,7 @@ hipError_t warm_stencil_tile(hipStream_t s) {
     p.nchunks = 1;  // nbands = 0: every wave returns at once
     hipLaunchKernelGGL((gol_tile<16, 16, false, false>), dim3(1), dim3(256), 0, s, nullptr, nullptr, p,
                        nullptr);
-    hipLaunchKernelGGL((gol_slab<16, 16, 8, false, false>), dim3(1), dim3(1024), 0, s, nullptr, nullptr, p,
+    hipLaunchKernelGGL((gol_slab<16, 16, 8, false, 0>), dim3(1), dim3(1024), 0, s, nullptr, nullptr, p,
                        nullptr);
     return hipGetLastError();
 }

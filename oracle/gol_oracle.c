@@ -86,6 +86,20 @@ static void *ref_calculate_next_state(void *arg) {
     return NULL;
 }
 
+typedef struct {
+    size_t bytes;
+    const uint8_t *src;
+    uint8_t *dst;
+} ref_copy_task;
+
+/* one server's gob-decoded private copy of the whole world: the servers are separate processes
+ * (broker/broker.go:58-66 calls them from one goroutine each), so their copies run concurrently */
+static void *ref_copy_world(void *arg) {
+    ref_copy_task *c = (ref_copy_task *)arg;
+    memcpy(c->dst, c->src, c->bytes);
+    return NULL;
+}
+
 /*
  * One reference turn: broker fan-out to `servers` strips (broker/broker.go:37-56), each
  * server splitting req.SplitSize rows over `threads` goroutines (server/server.go:83-97),
@@ -111,6 +125,20 @@ int oracle_ref_step(int n, const uint8_t *world, uint8_t *out, int threads, int 
     uint8_t ***server_world = (uint8_t ***)calloc((size_t)servers, sizeof(uint8_t **));
     uint8_t **server_block = (uint8_t **)calloc((size_t)servers, sizeof(uint8_t *));
 
+    if (fanout_copy) {
+        pthread_t *ctids = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)servers);
+        ref_copy_task *ct = (ref_copy_task *)malloc(sizeof(ref_copy_task) * (size_t)servers);
+        for (int s = 0; s < servers; s++) {
+            server_block[s] = (uint8_t *)malloc((size_t)n * n);
+            ct[s].bytes = (size_t)n * n;
+            ct[s].src = world;
+            ct[s].dst = server_block[s];
+            pthread_create(&ctids[s], NULL, ref_copy_world, &ct[s]);
+        }
+        for (int s = 0; s < servers; s++) pthread_join(ctids[s], NULL);
+        free(ctids);
+        free(ct);
+    }
     /* broker publish: splitSize := ImageSize / numServers (broker/broker.go:38-51) */
     int split = n / servers, diff = n % servers, pos = 0, nt = 0;
     for (int s = 0; s < servers; s++) {
@@ -119,9 +147,7 @@ int oracle_ref_step(int n, const uint8_t *world, uint8_t *out, int threads, int 
         if (diff != 0) { pos++; diff--; }
         pos++;
         uint8_t **w = rows;
-        if (fanout_copy) { /* the server's gob-decoded private copy of the whole world */
-            server_block[s] = (uint8_t *)malloc((size_t)n * n);
-            memcpy(server_block[s], world, (size_t)n * n);
+        if (fanout_copy) { /* the server's private copy of the whole world (made above) */
             server_world[s] = (uint8_t **)malloc(sizeof(uint8_t *) * (size_t)n);
             for (int y = 0; y < n; y++) server_world[s][y] = server_block[s] + (size_t)y * n;
             w = server_world[s];

@@ -128,29 +128,54 @@ def test_tracked_flips_small_board_graphs(golhip, oracle, monkeypatch):
         assert [tuple(c) for c in e.flips().tolist()] == oracle.flips(gen_prev, expected)
 
 
+@pytest.mark.parametrize("k,counts", [(8, True), (16, True), (16, False), (12, False)])
 @pytest.mark.parametrize("shape,strips", [((512, 512), 1), ((96, 640), 1), ((300, 1000), 2),
-                                          ((130, 4160), 4)])
-def test_step_flips_ring_every_turn(golhip, oracle, shape, strips):
+                                          ((130, 4160), 4), ((16, 16), 1), ((1000, 2000), 1)])
+def test_step_flips_ring_every_turn(golhip, oracle, shape, strips, k, counts):
     """golhip_step_flips: every turn's CellFlipped (turn by turn, row-major) and alive count from
     ONE extraction over the device ring of per-turn flips boards -- the TestSdl event stream
-    (sdl_test.go:57-74) -- equal to the oracle's per-turn diffs."""
+    (sdl_test.go:57-74) -- equal to the oracle's per-turn diffs.  Single-strip small boards fill
+    the ring with K-deep register-slab launches that write EVERY generation's flips (K = 8/12/16
+    slots per launch, the counting and non-counting slab shapes); strips and the tail of a call
+    use one-generation launches."""
     h, w = shape
     rng = np.random.default_rng(h * 3 + w + strips)
     board = ((rng.random(shape) < 0.4) * 255).astype(np.uint8)
-    with golhip.Engine(w, h, ngpus=1, k=8, strips=strips) as e:
+    with golhip.Engine(w, h, ngpus=1, k=k, strips=strips) as e:
         e.load(board)
         assert e.flips_ring_capacity() >= 40
         prev = oracle.to_cells(board)
-        for turns in (1, 17, 40):
-            per_turn, alive = e.step_flips(turns, counts=True)
+        for turns in (1, 17, 40, 33):
+            per_turn, alive = e.step_flips(turns, counts=counts)
             assert len(per_turn) == turns
             for t in range(turns):
                 cur, _ = oracle.packed_run(prev, 1)
                 assert [tuple(c) for c in per_turn[t].tolist()] == oracle.flips(prev, cur), (turns, t)
-                assert int(alive[t]) == int((cur == 255).sum())
+                if counts:
+                    assert int(alive[t]) == int((cur == 255).sum())
                 prev = cur
         assert np.array_equal(e.store(), prev)
         assert [tuple(c) for c in e.flips().tolist()] == [tuple(c) for c in per_turn[-1].tolist()]
+
+
+def test_step_flips_sdl_512_every_count(golhip, oracle):
+    """TestSdl (sdl_test.go:57-74,107-116): a shadow board toggled by every CellFlipped of 100
+    turns of images/512x512.pgm, its alive count at each TurnComplete equal to check/alive's CSV --
+    through 16-deep ring launches (gol_slab writing every generation's flips)."""
+    _, _, board = oracle.read_pgm(REF / "images/512x512.pgm")
+    csv = oracle.read_alive_csv(REF / "check/alive/512x512.csv")
+    shadow = (board == 255)
+    with golhip.Engine(512, 512, k=16) as e:
+        e.load(board)
+        assert e.launch_kind(16)[0] == "slab"
+        t0 = 0
+        for turns in (64, 36):
+            per_turn, _ = e.step_flips(turns)
+            for t, cells in enumerate(per_turn):
+                shadow[cells[:, 1], cells[:, 0]] ^= True
+                assert int(shadow.sum()) == csv[t0 + t + 1], t0 + t + 1
+            t0 += turns
+        assert np.array_equal(shadow * 255, e.store())
 
 
 def test_step_flips_capacity_errors(golhip, oracle):
