@@ -10,5 +10,7 @@ $G 600 $O/pytest_flips.log python -u -m pytest tests/test_gpu_parity.py -k "flip
 tail -1 $O/pytest_flips.log
 $G 300 $O/flips_profile.log python3 scripts/flips_profile.py || exit $?
 tail -1 $O/flips_profile.log
-$G 300 $O/rocprof_flips.log rocprofv3 --kernel-trace --hip-trace --stats -d $O/prof -o flips -- python3 scripts/flips_profile.py --calls 4 --snapshots 8 || exit $?
-find $O/prof -name "*stats*" | head -20
+# the raw traces exceed what gpurun copies back: keep only the stats summaries
+$G 300 $O/rocprof_flips.log rocprofv3 --kernel-trace --hip-trace --stats -d /tmp/prof_r03b -o flips -- python3 scripts/flips_profile.py --calls 4 --snapshots 8 || exit $?
+find /tmp/prof_r03b -name "*stats*.csv" -exec cp {} $O/ \;
+ls -la $O
