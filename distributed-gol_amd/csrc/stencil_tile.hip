@@ -114,6 +114,33 @@ struct TileStep {
     };
 };
 
+// Row sums handed to gen_rows instead of computed from c[] (gol_slab's exchange): NoPre computes
+// every row; SlabPre<S> supplies rows 0 and S + 1 (the neighbour waves' edge rows: sums and carries
+// only, they are never a centre row) and rows 1 and S (this wave's own edge rows, computed once
+// before the exchange that publishes them: sums, carries and centre cells).
+struct NoPre {
+    static constexpr bool has(int) { return false; }
+    template <int R>
+    __device__ __forceinline__ void get(std::integral_constant<int, R>, uint32_t &, uint32_t &,
+                                        uint32_t &) const {}
+};
+template <int S>
+struct SlabPre {
+    uint32_t ts, tcy;            // row 0 (above): the upper neighbour wave's last row
+    uint32_t fs, fcy, fctr;      // row 1: this wave's first row
+    uint32_t ls, lcy, lctr;      // row S: this wave's last row
+    uint32_t bs, bcy;            // row S + 1 (below): the lower neighbour wave's first row
+    static constexpr bool has(int r) { return r == 0 || r == 1 || r == S || r == S + 1; }
+    template <int R>
+    __device__ __forceinline__ void get(std::integral_constant<int, R>, uint32_t &s, uint32_t &cy,
+                                        uint32_t &ctr) const {
+        if constexpr (R == 0) s = ts, cy = tcy, ctr = 0u;
+        else if constexpr (R == 1) s = fs, cy = fcy, ctr = fctr;
+        else if constexpr (R == S) s = ls, cy = lcy, ctr = lctr;
+        else if constexpr (R == S + 1) s = bs, cy = bcy, ctr = 0u;
+    }
+};
+
 // One generation over rows [LO, LO + N) of c (compile time) from the previous generation's rows
 // [LO - 1, LO + N].  The rows are cut into NS segments that advance together, op-major (one op
 // of every segment, then the next op): NS independent dependency chains per wave.  A segment
@@ -125,22 +152,38 @@ struct TileStep {
 // top-down segment's last row takes the next segment's first m (saved then).
 // emit(integral_constant<r>, next, centre) sees every new row and the centre cells it replaces
 // (same drifted frame: the last generation's flips are next ^ centre).
-template <int LO, int N, bool WRITE, int NC = kTileChains, bool REV0 = false, int R, class F>
-__device__ __forceinline__ void gen_rows(uint32_t (&c)[R], F &&emit) {
+template <int LO, int N, bool WRITE, int NC = kTileChains, bool REV0 = false, int R, class F,
+          class P = NoPre>
+__device__ __forceinline__ void gen_rows(uint32_t (&c)[R], F &&emit, const P &pre = P{}) {
     constexpr int NS = N < NC ? N : NC;
     using TS0 = TileStep<LO, N, NS, REV0, 0>;
+    static_assert(!REV0 || !P::has(LO - 1), "precomputed sums: top-down segments only");
     constexpr int L = (N + NS - 1) / NS;
     uint32_t os[NS], ocy[NS], ms[NS], mcy[NS], mc[NS], ss[NS], scy[NS];
     {
+        // the initial (o, m) rows of every segment; rows the provider holds are not recomputed
+        auto init_row = [](int i) constexpr {
+            const int sg = i / 2;
+            return (i & 1) ? (TS0::rev(sg) ? TS0::first(sg + 1) - 1 : TS0::first(sg))
+                           : (TS0::rev(sg) ? TS0::first(sg + 1) : TS0::first(sg) - 1);
+        };
+        struct Need {
+            constexpr bool operator()(int i) const {
+                const int sg = i / 2;
+                const int r = (i & 1) ? (TS0::rev(sg) ? TS0::first(sg + 1) - 1 : TS0::first(sg))
+                                      : (TS0::rev(sg) ? TS0::first(sg + 1) : TS0::first(sg) - 1);
+                return !P::has(r);
+            }
+        };
         uint32_t x[2 * NS], s2[2 * NS], cy2[2 * NS], c2[2 * NS];
 #pragma unroll
-        for (int sg = 0; sg < NS; ++sg) {
-            // top-down: o = the row above the first, m = the first; bottom-up: o = the row below
-            // the last (the next segment's first row, still unwritten here), m = the last
-            x[2 * sg] = TS0::rev(sg) ? c[TS0::first(sg + 1)] : c[TS0::first(sg) - 1];
-            x[2 * sg + 1] = TS0::rev(sg) ? c[TS0::first(sg + 1) - 1] : c[TS0::first(sg)];
-        }
-        sums_om<2 * NS>(x, s2, cy2, c2);
+        for (int i = 0; i < 2 * NS; ++i) x[i] = c[init_row(i)];
+        sums_om<2 * NS>(x, s2, cy2, c2, Need{});
+        static_for(std::make_integer_sequence<int, 2 * NS>{}, [&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            constexpr int r = init_row(i);
+            if constexpr (P::has(r)) pre.get(std::integral_constant<int, r>{}, s2[i], cy2[i], c2[i]);
+        });
 #pragma unroll
         for (int sg = 0; sg < NS; ++sg) {
             os[sg] = s2[2 * sg], ocy[sg] = cy2[2 * sg];
@@ -153,10 +196,21 @@ __device__ __forceinline__ void gen_rows(uint32_t (&c)[R], F &&emit) {
         using TS = TileStep<LO, N, NS, REV0, i>;
         constexpr typename TS::Active active{};
         constexpr typename TS::Fresh fresh{};
+        struct Compute {  // fresh rows whose sums are not precomputed
+            constexpr bool operator()(int sg) const {
+                return TS::fresh_row(sg) >= 0 && !P::has(TS::fresh_row(sg));
+            }
+        };
         uint32_t x[NS], bs[NS], bcy[NS], bc[NS], nx[NS];
 #pragma unroll
         for (int sg = 0; sg < NS; ++sg) x[sg] = fresh(sg) ? c[TS::fresh_row(sg)] : 0u;
-        sums_om<NS>(x, bs, bcy, bc, fresh);
+        sums_om<NS>(x, bs, bcy, bc, Compute{});
+        static_for(std::make_integer_sequence<int, NS>{}, [&](auto sgc) {
+            constexpr int sg = decltype(sgc)::value;
+            constexpr int fr = TS::fresh_row(sg);
+            if constexpr (fr >= 0 && P::has(fr))
+                pre.get(std::integral_constant<int, fr>{}, bs[sg], bcy[sg], bc[sg]);
+        });
 #pragma unroll
         for (int sg = 0; sg < NS; ++sg)
             if (active(sg) && !fresh(sg)) bs[sg] = ss[sg + 1], bcy[sg] = scy[sg + 1], bc[sg] = 0u;
@@ -300,8 +354,11 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
                                                    uint32_t *__restrict__ out, StencilParams p,
                                                    unsigned long long *__restrict__ slots) {
     constexpr int T = W * S - 2 * K;
-    static_assert(T >= 1 && K >= 2 && K <= 32 && W >= 2, "slab geometry");
-    __shared__ uint32_t ex[2][W][2][64];
+    static_assert(T >= 1 && K >= 2 && K <= 32 && W >= 2 && S >= 2, "slab geometry");
+    // the waves' edge-row SUMS (3-cell sum bits and carries of the first and last row), not the
+    // rows: a row's sums are computed once, by the wave that owns it, instead of also by the
+    // neighbour that needs them (2 of every S + 2 row sums per wave and generation)
+    __shared__ uint32_t ex[2][W][4][64];
     // per-generation alive counts of the slab, per lane (summed over the waves by LDS adds; one
     // global atomic per generation per slab at the end)
     // per-generation alive counts, one slot per wave and lane (plain LDS stores; twelve waves'
@@ -328,8 +385,9 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
     const int col = (colraw + p.wd) % p.wd;
     const int rowbytes = (int)(p.pitch * 4);
     uint32_t c[S + 2];
-    c[0] = c[S + 1] = 0;
+    c[0] = c[S + 1] = 0;  // never read: their sums come from the neighbour waves (pre)
     load_rows<1, S>(c, in, p, ya - K + w * S, col);
+    SlabPre<S> pre{};
     const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
         out + (int64_t)ya * p.pitch, 0, nrows * rowbytes, kBufferRsrcWord3);
     __amdgpu_buffer_rsrc_t drsrc = orsrc;
@@ -353,11 +411,21 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
     };
     auto exchange = [&](int g) {
         const int par = g & 1;
-        ex[par][w][0][lane] = c[1];
-        ex[par][w][1][lane] = c[S];
+        {  // this wave's edge rows' sums: published below and used by its own pass
+            uint32_t xr[2] = {c[1], c[S]}, s2[2], cy2[2], c2[2];
+            sums_om<2>(xr, s2, cy2, c2);
+            pre.fs = s2[0], pre.fcy = cy2[0], pre.fctr = c2[0];
+            pre.ls = s2[1], pre.lcy = cy2[1], pre.lctr = c2[1];
+        }
+        ex[par][w][0][lane] = pre.fs;
+        ex[par][w][1][lane] = pre.fcy;
+        ex[par][w][2][lane] = pre.ls;
+        ex[par][w][3][lane] = pre.lcy;
         lds_barrier();
-        c[0] = w > 0 ? ex[par][w - 1][1][lane] : 0u;
-        c[S + 1] = w < W - 1 ? ex[par][w + 1][0][lane] : 0u;
+        pre.ts = w > 0 ? ex[par][w - 1][2][lane] : 0u;
+        pre.tcy = w > 0 ? ex[par][w - 1][3][lane] : 0u;
+        pre.bs = w < W - 1 ? ex[par][w + 1][0][lane] : 0u;
+        pre.bcy = w < W - 1 ? ex[par][w + 1][1][lane] : 0u;
         if constexpr (COUNT && 2 * S <= K) {
             // Generation g - 2 (0-based) is complete in LDS after this barrier.  With 2S <= K,
             // waves 0 and W - 1 hold only halo rows, dead from generation S on (g_end below),
@@ -410,7 +478,7 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
                     golhip::store_row<1, false>(drsrc, ls, dv, rowoff);
                 }
             }
-        });
+        }, pre);
         if constexpr (CNT)
             cnt_lds[gen][w][lane] = count_lane ? cnt : 0u;
     };
@@ -548,13 +616,11 @@ hipError_t launch_slab_kws(const uint32_t *in, uint32_t *out, const StencilParam
 
 }  // namespace
 
-// (K, waves, rows per wave, interleaved row chains)
+// (K, waves, rows per wave, interleaved row chains): the production shapes (pick_reg_kernel) and
+// the tuning neighbours kept measurable (profiles/r03/small_boards_r03.txt)
 #define GOLHIP_SLAB_CONFIGS(X) \
-    X(8, 8, 4, 4) X(8, 8, 8, 4) X(8, 16, 4, 4) X(8, 16, 8, 4) X(12, 8, 8, 4) X(12, 16, 4, 4) \
-    X(12, 16, 8, 4) X(16, 8, 8, 4) X(16, 8, 10, 4) X(16, 8, 11, 4) X(16, 8, 12, 4) X(16, 8, 13, 4) \
-    X(16, 8, 14, 4) X(16, 8, 16, 4) X(16, 8, 20, 4) X(16, 8, 24, 4) X(16, 16, 4, 4) X(16, 16, 6, 4) \
-    X(16, 16, 8, 4) X(16, 16, 16, 4) X(16, 4, 16, 4) X(16, 4, 24, 4) X(16, 8, 12, 2) X(16, 8, 12, 3) \
-    X(16, 12, 8, 2) X(16, 12, 8, 4)
+    X(8, 8, 4, 4) X(8, 8, 8, 4) X(12, 8, 8, 4) X(16, 8, 8, 4) X(16, 8, 12, 4) X(16, 16, 8, 4) \
+    X(16, 8, 12, 2) X(16, 12, 8, 2) X(16, 12, 8, 4) X(16, 12, 7, 2) X(16, 10, 8, 2) X(16, 14, 6, 2)
 
 bool stencil_slab_flips_every_gen(int K, int W, int S, int NC) {
     return stencil_slab_supported(K, W, S, NC) && slab_prod_shape(K, W, S, NC);
