@@ -109,9 +109,18 @@ def parse():
     return ap.parse_args()
 
 
+def barrier():
+    """The ranks' barrier: on the GPUs through the RCCL process group when there is one (a gloo TCP
+    barrier inside a ~1 ms timed region would be a sizeable share of it)."""
+    if dist.get_backend() == "nccl":
+        dist.barrier(device_ids=[torch.cuda.current_device()])
+    else:
+        dist.barrier()
+
+
 def timed_steps(eng: golhip.Engine, steps: int, world: int) -> float:
     if world > 1:
-        dist.barrier()
+        barrier()
     torch.cuda.synchronize()
     eng.sync()
     t0 = time.perf_counter()
@@ -122,11 +131,12 @@ def timed_steps(eng: golhip.Engine, steps: int, world: int) -> float:
     # three engine streams before it only added ~10 us of host round trips to a 20-turn region
     torch.cuda.synchronize()
     if world > 1:
-        dist.barrier()
+        barrier()
     dt = time.perf_counter() - t0
     eng.sync()
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64)
+        t = torch.tensor([dt], dtype=torch.float64,
+                         device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     return dt
@@ -357,8 +367,6 @@ def main():
     if world != a.gpus:
         if world == 1 and a.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
-    if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
     # test hook (tests/test_gpu_rank_host.py): GOLHIP_HOST_COMM=1 runs the rank engines with the gloo
     # host transport instead of RCCL, so N ranks can share the one GPU of a test box (RCCL refuses
     # two ranks on one device); the engine, its launch plan and the timed region are unchanged
@@ -366,6 +374,12 @@ def main():
     if host_comm:
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
+    if world > 1:
+        # one process per GPU: the bench's own collectives (barriers, the max-over-ranks time, the
+        # RCCL id broadcast) over RCCL; gloo where RCCL cannot run (the host-transport hook's
+        # ranks share one GPU; CPU-only test runs)
+        backend = "nccl" if torch.cuda.is_available() and not host_comm else "gloo"
+        dist.init_process_group(backend, rank=rank, world_size=world)
 
     width = a.size
     height = a.height or a.size * world

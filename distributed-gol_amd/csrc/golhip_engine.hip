@@ -536,21 +536,48 @@ RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K, bool counting) 
     // counts and flush the other waves' per-generation sums during the launch (5120^2 with every
     // count 1.005 -> 0.998 us/turn, 4096^2 0.951 -> 0.939; without counts 8 x 12 stays faster,
     // 0.814 vs 0.848: profiles/r02/r02ab_slab_shapes.txt)
-    const int W = K == 16 && counting ? 12 : 8;
-    const int S = K == 16 ? (counting ? 8 : 12) : 8, NC = K == 16 ? 2 : 4;
-    if (!golhip::stencil_slab_supported(K, W, S, NC)) return rk;
-    const int64_t per = golhip::chunk_words(K, h->variant);
-    const int64_t nchunks = (h->wd + per - 1) / per;
-    const int64_t minband = std::max(K, 8);
-    const int64_t waves1 = (rows_total + minband - 1) / minband * nchunks;
     if (h->cus == 0) {
         hipDeviceProp_t prop;
         h->cus = hipGetDeviceProperties(&prop, h->shards[0].device) == hipSuccess
                      ? prop.multiProcessorCount
                      : 256;
     }
+    const int64_t per = golhip::chunk_words(K, h->variant);
+    const int64_t nchunks = (h->wd + per - 1) / per;
+    const int64_t minband = std::max(K, 8);
+    const int64_t waves1 = (rows_total + minband - 1) / minband * nchunks;
     if (waves1 > 16 * (int64_t)h->cus) return rk;
-    rk.kind = 3, rk.W = W, rk.S = S, rk.NC = NC, rk.T = W * S - 2 * K;
+    // K = 16: among the candidate shapes, the least modelled time: a slab is one workgroup per
+    // CU, and its time is set by the SIMD with the most rows to update each generation, ceil(W/4)
+    // waves x S rows, times the rounds of workgroups over the CUs.  The board decides: 5120^2
+    // keeps 12 x 8 (240 slabs; 12 x 7 would need 297 > 256 CUs), 4096^2 takes 12 x 7 (237 slabs,
+    // 21 rows per SIMD instead of 24): 0.926 -> 0.869 us/turn with every count, 0.791 -> 0.770
+    // without (profiles/r03/r03e_tune_slab.log).  Counting slabs keep 12 waves (2S <= K: the
+    // pure-halo waves flush the counts during the launch); without counts 8 x 12 measured best
+    // where it fits (5120^2: 0.801 vs 0.830 for 12 x 8).
+    struct Cand {
+        int W, S, NC;
+    };
+    static constexpr Cand kCount16[] = {{12, 8, 2}, {12, 7, 2}};
+    static constexpr Cand kPlain16[] = {{8, 12, 2}, {12, 7, 2}};
+    static constexpr Cand kOther[] = {{8, 8, 4}};
+    const Cand *cands = K == 16 ? (counting ? kCount16 : kPlain16) : kOther;
+    const int ncand = K == 16 ? 2 : 1;
+    double best = 1e300;
+    for (int i = 0; i < ncand; ++i) {
+        const Cand c = cands[i];
+        if (!golhip::stencil_slab_supported(K, c.W, c.S, c.NC)) continue;
+        const int64_t T = (int64_t)c.W * c.S - 2 * K;
+        if (T < 1) continue;
+        const int64_t slabs = (rows_total + T - 1) / T * ((h->wd + golhip::kTileChunkWords - 1) /
+                                                         golhip::kTileChunkWords);
+        const int64_t rounds = (slabs + h->cus - 1) / h->cus;
+        const double cost = (double)rounds * (double)((c.W + 3) / 4) * c.S;
+        if (cost < best) {  // ties keep the earlier (measured-preferred) shape
+            best = cost;
+            rk.kind = 3, rk.W = c.W, rk.S = c.S, rk.NC = c.NC, rk.T = (int)T;
+        }
+    }
     return rk;
 }
 

@@ -581,7 +581,8 @@ hipError_t launch_tile_kt(const uint32_t *in, uint32_t *out, const StencilParams
 // flips variant (LD = 2).
 constexpr bool slab_prod_shape(int K, int W, int S, int NC) {
     return (K == 16 && W == 8 && S == 12 && NC == 2) || (K == 16 && W == 12 && S == 8 && NC == 2) ||
-           (K == 8 && W == 8 && S == 8 && NC == 4) || (K == 12 && W == 8 && S == 8 && NC == 4);
+           (K == 16 && W == 12 && S == 7 && NC == 2) || (K == 8 && W == 8 && S == 8 && NC == 4) ||
+           (K == 12 && W == 8 && S == 8 && NC == 4);
 }
 
 template <int K, int W, int S, int NC>
