@@ -454,7 +454,7 @@ def test_register_tile_tracked_flips(golhip, oracle, monkeypatch, k):
 
 SLAB_CONFIGS = [(8, 8, 4), (8, 8, 8), (12, 8, 8), (16, 8, 8), (16, 8, 12), (16, 16, 8),
                 (16, 8, 12, 2), (16, 12, 8, 2), (16, 12, 8), (16, 12, 7, 2), (16, 10, 8, 2),
-                (16, 14, 6, 2)]
+                (16, 14, 6, 2), (16, 12, 6, 2)]
 
 
 @pytest.mark.parametrize("cfg", SLAB_CONFIGS)
@@ -465,7 +465,8 @@ def test_register_slab_kernel(golhip, oracle, monkeypatch, cfg):
     k, waves, rows = cfg[:3]
     code = (cfg[3] * 10000 if len(cfg) > 3 else 0) + waves * 100 + rows
     monkeypatch.setenv("GOLHIP_SLAB", str(code))
-    for (h, w) in [(77, 640), (16, 16), (5, 96), (300, 4160), (129, 200), (40, 8192), (250, 1984)]:
+    for (h, w) in [(77, 640), (16, 16), (5, 96), (300, 4160), (129, 200), (40, 8192), (250, 1984),
+                   (100, 4096)]:
         rng = np.random.default_rng(h * 7 + w + k + waves + rows)
         board = ((rng.random((h, w)) < 0.4) * 255).astype(np.uint8)
         turns = 3 * k + 1
