@@ -512,10 +512,8 @@ RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K, bool counting) 
     // an explicit level split or band height (tests, tuning) asks for the streaming kernels
     const bool forced = h->force_tile > 0 || h->force_slab > 0;
     if (!forced && (h->force_split > 0 || h->band_rows > 0)) return rk;
-    // the input descriptor spans the board's rows; offsets are 32-bit, and a packed narrow chunk
-    // (slab_seg) stores through one descriptor over all output rows, whose dropped stores sit at
-    // kOutOfRange = 2^30 past it
-    if ((int64_t)h->height * h->pitch * 4 >= ((int64_t)1 << 30)) return rk;
+    // the input descriptor spans the board's rows; offsets are 32-bit signed
+    if ((int64_t)h->height * h->pitch * 4 >= ((int64_t)1 << 31)) return rk;
     if (h->force_tile > 0) {
         if (golhip::stencil_tile_supported(K, h->force_tile)) rk.kind = 2, rk.T = h->force_tile;
         return rk;
@@ -560,19 +558,19 @@ RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K, bool counting) 
     struct Cand {
         int W, S, NC;
     };
-    static constexpr Cand kCount16[] = {{12, 8, 2}, {12, 7, 2}, {12, 6, 2}};
-    static constexpr Cand kPlain16[] = {{8, 12, 2}, {12, 7, 2}, {12, 6, 2}};
+    static constexpr Cand kCount16[] = {{12, 8, 2}, {12, 7, 2}};
+    static constexpr Cand kPlain16[] = {{8, 12, 2}, {12, 7, 2}};
     static constexpr Cand kOther[] = {{8, 8, 4}};
     const Cand *cands = K == 16 ? (counting ? kCount16 : kPlain16) : kOther;
-    const int ncand = K == 16 ? 3 : 1;
+    const int ncand = K == 16 ? 2 : 1;
     double best = 1e300;
     for (int i = 0; i < ncand; ++i) {
         const Cand c = cands[i];
         if (!golhip::stencil_slab_supported(K, c.W, c.S, c.NC)) continue;
         const int64_t T = (int64_t)c.W * c.S - 2 * K;
         if (T < 1) continue;
-        const int32_t nch = (int32_t)((h->wd + golhip::kTileChunkWords - 1) / golhip::kTileChunkWords);
-        const int64_t slabs = golhip::slab_groups((rows_total + T - 1) / T, h->wd, nch);
+        const int64_t slabs = (rows_total + T - 1) / T * ((h->wd + golhip::kTileChunkWords - 1) /
+                                                         golhip::kTileChunkWords);
         const int64_t rounds = (slabs + h->cus - 1) / h->cus;
         const double cost = (double)rounds * (double)((c.W + 3) / 4) * c.S;
         if (cost < best) {  // ties keep the earlier (measured-preferred) shape

@@ -134,27 +134,6 @@ bool stencil_slab_supported(int K, int W, int S, int NC = 4);
 bool stencil_slab_flips_every_gen(int K, int W, int S, int NC = 4);
 hipError_t warm_stencil_tile(hipStream_t s);
 constexpr int kTileChunkWords = 62;
-// gol_slab's narrow last column chunk: when the last chunk's words plus its two halo lanes fit at
-// least twice into a wave (segw <= 32), its slabs are packed nseg per wave -- lane segment k of
-// segw lanes works band (i * nseg + k) of that chunk -- instead of one 64-lane wave per slab with
-// most lanes idle (4096 wide = 128 words = 62 + 62 + 4: the third chunk packs 10 bands per wave).
-struct SlabSeg {
-    int segw, nseg;  // nseg == 1: no packing
-};
-__host__ __device__ inline SlabSeg slab_seg(int32_t wd, int32_t nchunks) {
-    const int wlast = wd - kTileChunkWords * (nchunks - 1);
-    const int segw = wlast + 2, nseg = 64 / segw;
-    return nseg >= 2 ? SlabSeg{segw, nseg} : SlabSeg{64, 1};
-}
-// Workgroups of a slab launch: nbands x (full chunks) + the packed last chunk's.
-__host__ __device__ inline int64_t slab_groups_main(int64_t nbands, int32_t wd, int32_t nchunks) {
-    return nbands * (slab_seg(wd, nchunks).nseg > 1 ? nchunks - 1 : nchunks);
-}
-__host__ __device__ inline int64_t slab_groups(int64_t nbands, int32_t wd, int32_t nchunks) {
-    const SlabSeg sg = slab_seg(wd, nchunks);
-    return slab_groups_main(nbands, wd, nchunks) +
-           (sg.nseg > 1 ? (nbands + sg.nseg - 1) / sg.nseg : 0);
-}
 // Words per column chunk of the level-split kernel (half-word halo for K <= 16).
 __host__ __device__ constexpr int split_chunk_words(int K) { return K <= 16 ? 63 : 62; }
 // Resident waves per CU of the stencil launch (occupancy query), for sizing the grid.

@@ -349,104 +349,53 @@ __device__ __forceinline__ uint32_t realign_drift_rt(uint32_t v, int g) {
 // p.diff + g * p.diff_stride (golhip_step_flips: one K-deep launch fills K slots of the per-turn
 // flips ring; the output rows are valid at every generation of the trapezoid, and each
 // generation's new row and the centre cells it replaces sit in the same drifted frame).
-// Input rows for lanes that each work their own band (gol_slab's packed narrow chunk): per-lane
-// row index and wrap, the row offset in the VGPR offset.
-template <int FIRST, int NROWS, int R>
-__device__ __forceinline__ void load_rows_lane(uint32_t (&c)[R], const uint32_t *in,
-                                               const StencilParams &p, int row0, int col) {
-    const int rowbytes = (int)(p.pitch * 4);
-    const int base_row = p.wrap_rows > 0 ? 0 : (int)p.lo;
-    const int span_rows = p.wrap_rows > 0 ? (int)p.wrap_rows : (int)(p.hi - p.lo);
-    const __amdgpu_buffer_rsrc_t irsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint32_t *>(in + (int64_t)base_row * p.pitch), 0, span_rows * rowbytes,
-        kBufferRsrcWord3);
-    const int wrap = (int)p.wrap_rows, lo = (int)p.lo, hi = (int)p.hi;
-    int ly = row0;
-    if (wrap > 0) {
-        ly %= wrap;
-        if (ly < 0) ly += wrap;
-    } else {
-        ly = ly < lo ? lo : (ly >= hi ? hi - 1 : ly);
-    }
-#pragma unroll
-    for (int r = 0; r < NROWS; ++r) {
-        c[FIRST + r] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(
-            irsrc, col * 4 + (ly - base_row) * rowbytes, 0, 0);
-        const int nx = ly + 1;
-        ly = wrap > 0 ? (nx == wrap ? 0 : nx) : (nx < hi ? nx : hi - 1);
-    }
-}
-
-// gol_slab: the register tile spread over the W waves of a workgroup.  Wave w holds S rows of the
-// slab's W*S (a 62-word column chunk, rows ya - K + wS ...) in c[1..S]; each generation the waves
-// swap their edge rows' sums through LDS (double-buffered by generation parity: one barrier per
-// generation) and update their S rows.  The trapezoid is paid once per slab (2K rows of W*S)
-// instead of once per wave, with S-row waves: more waves per SIMD at the same work.  Output: the
-// T = W*S - 2K middle rows.
-// LD: 0 no flips, 1 the last generation's flips to p.diff, 2 EVERY generation's flips to
-// p.diff + g * p.diff_stride (golhip_step_flips: one K-deep launch fills K slots of the per-turn
-// flips ring; the output rows are valid at every generation of the trapezoid, and each
-// generation's new row and the centre cells it replaces sit in the same drifted frame).
-// SEGM: a workgroup of the packed narrow last chunk (slab_seg): lane segment k (segw lanes: west
-// halo, the chunk's words, east halo) works band gidx * nseg + k, so rows, output offsets and the
-// "mine" tests are per lane; the generation code is the same.
-template <int K, int W, int S, bool COUNT, int LD, int NC, bool SEGM>
-__device__ __forceinline__ void slab_body(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
-                                          const StencilParams &p, unsigned long long *__restrict__ slots,
-                                          int64_t group, int64_t gidx, uint32_t (&ex)[2][W][4][64],
-                                          uint32_t (&cnt_lds)[COUNT ? K : 1][COUNT ? W : 1][64]) {
+template <int K, int W, int S, bool COUNT, int LD, int NC = kTileChains>
+__global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ in,
+                                                   uint32_t *__restrict__ out, StencilParams p,
+                                                   unsigned long long *__restrict__ slots) {
+    constexpr int T = W * S - 2 * K;
+    static_assert(T >= 1 && K >= 2 && K <= 32 && W >= 2 && S >= 2, "slab geometry");
+    // the waves' edge-row SUMS (3-cell sum bits and carries of the first and last row), not the
+    // rows: a row's sums are computed once, by the wave that owns it, instead of also by the
+    // neighbour that needs them (2 of every S + 2 row sums per wave and generation)
+    __shared__ uint32_t ex[2][W][4][64];
+    // per-generation alive counts of the slab, per lane (summed over the waves by LDS adds; one
+    // global atomic per generation per slab at the end)
+    // per-generation alive counts, one slot per wave and lane (plain LDS stores; twelve waves'
+    // atomic adds to ONE slot per lane serialised in the LDS pipe in front of every barrier),
+    // summed over the waves by the flushing wave
+    __shared__ uint32_t cnt_lds[COUNT ? K : 1][COUNT ? W : 1][64];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int rowbytes = (int)(p.pitch * 4);
-    int ya, yb, colraw, j, segw = 64;
-    bool active = true;
-    if constexpr (SEGM) {
-        const SlabSeg sg = slab_seg(p.wd, p.nchunks);
-        segw = sg.segw;
-        const int seg = lane / segw;
-        j = lane - seg * segw;
-        const int64_t bandi = gidx * sg.nseg + seg;
-        active = seg < sg.nseg && bandi < p.nbands;
-        band_rows(p, active ? bandi : 0, ya, yb);
-        if (!active) yb = ya;  // no rows of its own: never mine, never counted
-        colraw = (p.nchunks - 1) * kTileChunkWords + j - 1;
-    } else {
-        const int nch = slab_seg(p.wd, p.nchunks).nseg > 1 ? p.nchunks - 1 : p.nchunks;
-        const int64_t chunk = gidx % nch;
-        const int64_t bandi = gidx / nch;
-        band_rows(p, bandi, ya, yb);  // yb - ya <= T (the host sets p.band = T)
-        j = lane;
-        colraw = (int)chunk * kTileChunkWords + lane - 1;
-    }
+    // XCD-aware order: the dispatcher deals workgroups round-robin over the 8 XCDs (each with its
+    // own L2), so workgroup b runs on XCD b % 8.  Give XCD x a contiguous range of slabs (all
+    // column chunks of consecutive bands): the halo rows and halo lanes a slab reads were written
+    // by its neighbours in the previous launch on the SAME XCD, i.e. they hit that L2, except at
+    // the 8 range seams.
+    const int64_t ngroups = p.nbands * (int64_t)p.nchunks;
+    const int64_t per_xcd = (ngroups + kXcds - 1) / kXcds;
+    const int64_t group = (int64_t)(blockIdx.x % kXcds) * per_xcd + blockIdx.x / kXcds;
+    if (group >= ngroups) return;  // whole workgroup (grid padded to whole XCD rounds)
+    const int64_t chunk = group % p.nchunks;
+    const int64_t bandi = group / p.nchunks;
+    int ya, yb;
+    band_rows(p, bandi, ya, yb);  // yb - ya <= T (the host sets p.band = T)
     const int nrows = yb - ya;
+    const int colraw = (int)chunk * kTileChunkWords + lane - 1;
     const int col = (colraw + p.wd) % p.wd;
+    const int rowbytes = (int)(p.pitch * 4);
     uint32_t c[S + 2];
     c[0] = c[S + 1] = 0;  // never read: their sums come from the neighbour waves (pre)
-    if constexpr (SEGM)
-        load_rows_lane<1, S>(c, in, p, ya - K + w * S, col);
-    else
-        load_rows<1, S>(c, in, p, ya - K + w * S, col);
+    load_rows<1, S>(c, in, p, ya - K + w * S, col);
     SlabPre<S> pre{};
-    // output descriptors: a packed workgroup's lanes store to their own bands, so its descriptor
-    // spans every output row and the row base goes into the per-lane offset
-    const int out_span = (int)std::max(p.r0e, p.r1e);
-    const int rowbase = SEGM ? ya * rowbytes : 0;
     const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
-        out + (SEGM ? 0 : (int64_t)ya * p.pitch), 0, (SEGM ? out_span : nrows) * rowbytes,
-        kBufferRsrcWord3);
+        out + (int64_t)ya * p.pitch, 0, nrows * rowbytes, kBufferRsrcWord3);
     __amdgpu_buffer_rsrc_t drsrc = orsrc;
     if constexpr (LD == 1)
-        drsrc = __builtin_amdgcn_make_buffer_rsrc(p.diff + (SEGM ? 0 : (int64_t)ya * p.pitch), 0,
-                                                  (SEGM ? out_span : nrows) * rowbytes,
-                                                  kBufferRsrcWord3);
-    // lanes 1 .. segw - 2 of a segment own their word, 2 .. segw - 1 hold the drift count window
-    LaneStore ls;
-    if (SEGM) {
-        if (active && j >= 1 && j <= segw - 2 && colraw < p.wd) ls.off_full = col * 4, ls.own_mask = ~0u;
-    } else {
-        ls = lane_store<false>(lane, colraw, col, p.wd);
-    }
-    const bool count_lane = active && j >= 2 && colraw <= p.wd;
+        drsrc = __builtin_amdgcn_make_buffer_rsrc(p.diff + (int64_t)ya * p.pitch, 0,
+                                                  nrows * rowbytes, kBufferRsrcWord3);
+    const LaneStore ls = lane_store<false>(lane, colraw, col, p.wd);
+    const bool count_lane = lane >= 2 && colraw <= p.wd;
     // slab row of c[1]: output row o = w*S + (r - 1) - K is this band's if 0 <= o < nrows
     const int o0 = w * S - K;
     if constexpr (COUNT)
@@ -493,42 +442,33 @@ __device__ __forceinline__ void slab_body(const uint32_t *__restrict__ in, uint3
     };
     // FULL: every row of this wave is an output row of the band (interior waves): the counts need
     // no per-row mask (one v_bcnt per row instead of a select and a v_bcnt)
+    const bool full = o0 >= 0 && o0 + S <= nrows;
     // HALO: no row of this wave is an output row of the band (the slab's K-row halos, or rows past
     // a short last band): it never counts and never stores, so it skips the last generation, and
     // any generation at which all its rows are already outside the trapezoid [g, W*S - g)
-    // (packed workgroups: over all active lanes' bands; inactive lanes never count or store)
-    bool full, halo;
-    if constexpr (SEGM) {
-        full = o0 >= 0 && __ballot(active && o0 + S > nrows) == 0ull;
-        halo = o0 + S <= 0 || __ballot(active && o0 < nrows) == 0ull;
-    } else {
-        full = o0 >= 0 && o0 + S <= nrows;
-        halo = o0 + S <= 0 || o0 >= nrows;
-    }
+    const bool halo = o0 + S <= 0 || o0 >= nrows;
     auto pass = [&](auto last_c, auto full_c, auto cnt_c, int gen) {
         constexpr bool LAST = decltype(last_c)::value, FULL = decltype(full_c)::value;
         constexpr bool CNT = COUNT && decltype(cnt_c)::value;
         uint32_t cnt = 0;
         __amdgpu_buffer_rsrc_t grsrc = orsrc;  // LD == 2: this generation's flips ring slot
         if constexpr (LD == 2)
-            grsrc = __builtin_amdgcn_make_buffer_rsrc(
-                p.diff + gen * p.diff_stride + (SEGM ? 0 : (int64_t)ya * p.pitch), 0,
-                (SEGM ? out_span : nrows) * rowbytes, kBufferRsrcWord3);
+            grsrc = __builtin_amdgcn_make_buffer_rsrc(p.diff + gen * p.diff_stride + (int64_t)ya * p.pitch,
+                                                      0, nrows * rowbytes, kBufferRsrcWord3);
         // (segment 0 bottom-up, REV0 -- the hand-off row above needed only at its last step --
         // measured 3-7 % slower: profiles/r02/small_boards.txt)
         gen_rows<1, S, !LAST, NC>(c, [&](auto rc, uint32_t nx, uint32_t centre) {
             constexpr int r = decltype(rc)::value;
             const int o = o0 + r - 1;
-            // wave-uniform, except in a packed workgroup (each lane's own band)
-            const bool mine = FULL || (o >= 0 && o < nrows);
+            const bool mine = FULL || (o >= 0 && o < nrows);  // wave-uniform
             if (CNT) cnt += __builtin_popcount(mine ? nx : 0u);
             if constexpr (LD == 2) {  // every generation's flips (output rows only)
                 Words<1> dv;
                 dv.w[0] = realign_drift_rt(nx ^ centre, gen);
-                golhip::store_row<1, false>(grsrc, ls, dv, mine ? rowbase + o * rowbytes : kOutOfRange);
+                golhip::store_row<1, false>(grsrc, ls, dv, mine ? o * rowbytes : kOutOfRange);
             }
             if constexpr (LAST) {
-                const int rowoff = mine ? rowbase + o * rowbytes : kOutOfRange;
+                const int rowoff = mine ? o * rowbytes : kOutOfRange;
                 Words<1> v;
                 v.w[0] = realign_drift<K>(nx);
                 golhip::store_row<1, false>(orsrc, ls, v, rowoff);
@@ -611,41 +551,12 @@ __device__ __forceinline__ void slab_body(const uint32_t *__restrict__ in, uint3
                 flush_counts<1>(acc, K - 1, lane, group, slots);
             }
         } else {
-            for (int jj = w; jj < K; jj += W) {
-                uint32_t acc[1] = {cnt_sum(jj)};
-                flush_counts<1>(acc, jj, lane, group, slots);
+            for (int j = w; j < K; j += W) {
+                uint32_t acc[1] = {cnt_sum(j)};
+                flush_counts<1>(acc, j, lane, group, slots);
             }
         }
     }
-}
-
-template <int K, int W, int S, bool COUNT, int LD, int NC = kTileChains>
-__global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ in,
-                                                   uint32_t *__restrict__ out, StencilParams p,
-                                                   unsigned long long *__restrict__ slots) {
-    static_assert(W * S - 2 * K >= 1 && K >= 2 && K <= 32 && W >= 2 && S >= 2, "slab geometry");
-    // the waves' edge-row SUMS (3-cell sum bits and carries of the first and last row), not the
-    // rows: a row's sums are computed once, by the wave that owns it, instead of also by the
-    // neighbour that needs them (2 of every S + 2 row sums per wave and generation)
-    __shared__ uint32_t ex[2][W][4][64];
-    // per-generation alive counts, one slot per wave and lane (plain LDS stores; twelve waves'
-    // atomic adds to ONE slot per lane serialised in the LDS pipe in front of every barrier),
-    // summed over the waves by the flushing wave
-    __shared__ uint32_t cnt_lds[COUNT ? K : 1][COUNT ? W : 1][64];
-    // XCD-aware order: the dispatcher deals workgroups round-robin over the 8 XCDs (each with its
-    // own L2), so workgroup b runs on XCD b % 8.  Give XCD x a contiguous range of slabs (all
-    // column chunks of consecutive bands): the halo rows and halo lanes a slab reads were written
-    // by its neighbours in the previous launch on the SAME XCD, i.e. they hit that L2, except at
-    // the 8 range seams.  The packed narrow chunk's workgroups come last.
-    const int64_t nmain = slab_groups_main(p.nbands, p.wd, p.nchunks);
-    const int64_t ngroups = slab_groups(p.nbands, p.wd, p.nchunks);
-    const int64_t per_xcd = (ngroups + kXcds - 1) / kXcds;
-    const int64_t group = (int64_t)(blockIdx.x % kXcds) * per_xcd + blockIdx.x / kXcds;
-    if (group >= ngroups) return;  // whole workgroup (grid padded to whole XCD rounds)
-    if (group < nmain)
-        slab_body<K, W, S, COUNT, LD, NC, false>(in, out, p, slots, group, group, ex, cnt_lds);
-    else
-        slab_body<K, W, S, COUNT, LD, NC, true>(in, out, p, slots, group, group - nmain, ex, cnt_lds);
 }
 
 template <int K, int T>
@@ -670,15 +581,14 @@ hipError_t launch_tile_kt(const uint32_t *in, uint32_t *out, const StencilParams
 // flips variant (LD = 2).
 constexpr bool slab_prod_shape(int K, int W, int S, int NC) {
     return (K == 16 && W == 8 && S == 12 && NC == 2) || (K == 16 && W == 12 && S == 8 && NC == 2) ||
-           (K == 16 && W == 12 && S == 7 && NC == 2) || (K == 16 && W == 12 && S == 6 && NC == 2) ||
-           (K == 8 && W == 8 && S == 8 && NC == 4) ||
+           (K == 16 && W == 12 && S == 7 && NC == 2) || (K == 8 && W == 8 && S == 8 && NC == 4) ||
            (K == 12 && W == 8 && S == 8 && NC == 4);
 }
 
 template <int K, int W, int S, int NC>
 hipError_t launch_slab_kws(const uint32_t *in, uint32_t *out, const StencilParams &p,
                            unsigned long long *slots, hipStream_t s) {
-    const int64_t ngroups = slab_groups(p.nbands, p.wd, p.nchunks);
+    const int64_t ngroups = p.nbands * (int64_t)p.nchunks;
     const unsigned blocks = (unsigned)std::max<int64_t>(1, (ngroups + kXcds - 1) / kXcds * kXcds);
     const dim3 block(64 * W);
     if (p.diff && p.diff_stride > 0) {
@@ -711,8 +621,7 @@ hipError_t launch_slab_kws(const uint32_t *in, uint32_t *out, const StencilParam
 // the tuning neighbours kept measurable (profiles/r03/small_boards_r03.txt)
 #define GOLHIP_SLAB_CONFIGS(X) \
     X(8, 8, 4, 4) X(8, 8, 8, 4) X(12, 8, 8, 4) X(16, 8, 8, 4) X(16, 8, 12, 4) X(16, 16, 8, 4) \
-    X(16, 8, 12, 2) X(16, 12, 8, 2) X(16, 12, 8, 4) X(16, 12, 7, 2) X(16, 10, 8, 2) X(16, 14, 6, 2) \
-    X(16, 12, 6, 2)
+    X(16, 8, 12, 2) X(16, 12, 8, 2) X(16, 12, 8, 4) X(16, 12, 7, 2) X(16, 10, 8, 2) X(16, 14, 6, 2)
 
 bool stencil_slab_flips_every_gen(int K, int W, int S, int NC) {
     return stencil_slab_supported(K, W, S, NC) && slab_prod_shape(K, W, S, NC);

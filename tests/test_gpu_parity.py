@@ -454,7 +454,7 @@ def test_register_tile_tracked_flips(golhip, oracle, monkeypatch, k):
 
 SLAB_CONFIGS = [(8, 8, 4), (8, 8, 8), (12, 8, 8), (16, 8, 8), (16, 8, 12), (16, 16, 8),
                 (16, 8, 12, 2), (16, 12, 8, 2), (16, 12, 8), (16, 12, 7, 2), (16, 10, 8, 2),
-                (16, 14, 6, 2), (16, 12, 6, 2)]
+                (16, 14, 6, 2)]
 
 
 @pytest.mark.parametrize("cfg", SLAB_CONFIGS)
