@@ -339,6 +339,14 @@ __device__ __forceinline__ uint32_t realign_drift_rt(uint32_t v, int g) {
     return __builtin_amdgcn_alignbit(lane_from_east(v), v, (uint32_t)(g + 1));
 }
 
+// popcount(x) + acc as ONE v_bcnt_u32_b32 (the compiler splits a row sum of popcounts into
+// v_bcnt(x, 0) + v_add3 trees: 3 extra VALU per 8 rows)
+__device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
+    uint32_t r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+    return r;
+}
+
 // gol_slab: the register tile spread over the W waves of a workgroup.  Wave w holds S rows of the
 // slab's W*S (a 62-word column chunk, rows ya - K + wS ...) in c[1..S]; each generation the waves
 // swap their edge rows through LDS (c[0] = the row above, c[S+1] = the row below, double-buffered
@@ -357,8 +365,11 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
     static_assert(T >= 1 && K >= 2 && K <= 32 && W >= 2 && S >= 2, "slab geometry");
     // the waves' edge-row SUMS (3-cell sum bits and carries of the first and last row), not the
     // rows: a row's sums are computed once, by the wave that owns it, instead of also by the
-    // neighbour that needs them (2 of every S + 2 row sums per wave and generation)
-    __shared__ uint32_t ex[2][W][4][64];
+    // neighbour that needs them (2 of every S + 2 row sums per wave and generation).  Wave w's
+    // block is ex[par][w + 1]; blocks 0 and W + 1 stay zero, so the first and last wave read their
+    // missing neighbour's sums from there without a branch, and every address of a wave's exchange
+    // is one base (its upper neighbour's block) plus an immediate offset.
+    __shared__ uint32_t ex[2][W + 2][4][64];
     // per-generation alive counts of the slab, per lane (summed over the waves by LDS adds; one
     // global atomic per generation per slab at the end)
     // per-generation alive counts, one slot per wave and lane (plain LDS stores; twelve waves'
@@ -400,6 +411,15 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
     const int o0 = w * S - K;
     if constexpr (COUNT)
         for (int j = 0; j < K; ++j) cnt_lds[j][w][lane] = 0;  // halo waves never write theirs
+    if (w == 0)  // the zero neighbour blocks (ordered before any read by the first exchange's barrier)
+        for (int par = 0; par < 2; ++par)
+            for (int i = 0; i < 4; ++i) ex[par][0][i][lane] = ex[par][W + 1][i][lane] = 0u;
+    // exchange addressing: parity 0's base and the distance to parity 1 (words)
+    uint32_t *const ex_base0 = &ex[0][w][0][lane];
+    constexpr int kExPar = (W + 2) * 4 * 64;
+    // this wave's per-generation count slot: cnt_my[gen * W * 64] (unmasked; the flusher masks the
+    // lanes outside the count window once per generation)
+    uint32_t *const cnt_my = &cnt_lds[0][w][lane];
     // LDS-only barrier: the waves' global stores and count atomics stay in flight (a
     // __syncthreads() would also drain vmcnt every generation)
     auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
@@ -407,7 +427,7 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
         uint32_t a = 0;
 #pragma unroll
         for (int ww = 0; ww < W; ++ww) a += cnt_lds[j][ww][lane];
-        return a;
+        return count_lane ? a : 0u;
     };
     auto exchange = [&](int g) {
         const int par = g & 1;
@@ -417,15 +437,16 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
             pre.fs = s2[0], pre.fcy = cy2[0], pre.fctr = c2[0];
             pre.ls = s2[1], pre.lcy = cy2[1], pre.lctr = c2[1];
         }
-        ex[par][w][0][lane] = pre.fs;
-        ex[par][w][1][lane] = pre.fcy;
-        ex[par][w][2][lane] = pre.ls;
-        ex[par][w][3][lane] = pre.lcy;
+        uint32_t *const b = ex_base0 + par * kExPar;  // block w (the upper neighbour's)
+        b[256] = pre.fs;  // own block w + 1
+        b[320] = pre.fcy;
+        b[384] = pre.ls;
+        b[448] = pre.lcy;
         lds_barrier();
-        pre.ts = w > 0 ? ex[par][w - 1][2][lane] : 0u;
-        pre.tcy = w > 0 ? ex[par][w - 1][3][lane] : 0u;
-        pre.bs = w < W - 1 ? ex[par][w + 1][0][lane] : 0u;
-        pre.bcy = w < W - 1 ? ex[par][w + 1][1][lane] : 0u;
+        pre.ts = b[128];  // the upper neighbour's last row (zero block above wave 0)
+        pre.tcy = b[192];
+        pre.bs = b[512];  // the lower neighbour's first row (zero block below wave W - 1)
+        pre.bcy = b[576];
         if constexpr (COUNT && 2 * S <= K) {
             // Generation g - 2 (0-based) is complete in LDS after this barrier.  With 2S <= K,
             // waves 0 and W - 1 hold only halo rows, dead from generation S on (g_end below),
@@ -461,7 +482,7 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
             constexpr int r = decltype(rc)::value;
             const int o = o0 + r - 1;
             const bool mine = FULL || (o >= 0 && o < nrows);  // wave-uniform
-            if (CNT) cnt += __builtin_popcount(mine ? nx : 0u);
+            if (CNT) cnt = bcnt_acc(mine ? nx : 0u, cnt);
             if constexpr (LD == 2) {  // every generation's flips (output rows only)
                 Words<1> dv;
                 dv.w[0] = realign_drift_rt(nx ^ centre, gen);
@@ -479,8 +500,7 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
                 }
             }
         }, pre);
-        if constexpr (CNT)
-            cnt_lds[gen][w][lane] = count_lane ? cnt : 0u;
+        if constexpr (CNT) cnt_my[gen * (W * 64)] = cnt;
     };
     using No = std::false_type;
     using Yes = std::true_type;
