@@ -552,17 +552,18 @@ RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K, bool counting) 
     // waves x S rows, times the rounds of workgroups over the CUs.  The board decides: 5120^2
     // keeps 12 x 8 (240 slabs; 12 x 7 would need 297 > 256 CUs), 4096^2 takes 12 x 7 (237 slabs,
     // 21 rows per SIMD instead of 24): 0.926 -> 0.869 us/turn with every count, 0.791 -> 0.770
-    // without (profiles/r03/r03e_tune_slab.log).  Counting slabs keep 12 waves (2S <= K: the
-    // pure-halo waves flush the counts during the launch); without counts 8 x 12 measured best
-    // where it fits (5120^2: 0.801 vs 0.830 for 12 x 8).
+    // without (profiles/r03/r03e_tune_slab.log).  Ties keep the earlier shape: 8 x 12 measured
+    // best at 5120^2 with and without counts once the counting loop lost its add3 tree and the
+    // exchange its branches (0.916 vs 0.931 us/turn for 12 x 8 with every count, 0.806 vs 0.828
+    // without: profiles/r03/r03k_tune_slab.log).
     struct Cand {
         int W, S, NC;
     };
-    static constexpr Cand kCount16[] = {{12, 8, 2}, {12, 7, 2}};
+    static constexpr Cand kCount16[] = {{8, 12, 2}, {12, 8, 2}, {12, 7, 2}};
     static constexpr Cand kPlain16[] = {{8, 12, 2}, {12, 7, 2}};
     static constexpr Cand kOther[] = {{8, 8, 4}};
     const Cand *cands = K == 16 ? (counting ? kCount16 : kPlain16) : kOther;
-    const int ncand = K == 16 ? 2 : 1;
+    const int ncand = K == 16 ? (counting ? 3 : 2) : 1;
     double best = 1e300;
     for (int i = 0; i < ncand; ++i) {
         const Cand c = cands[i];

@@ -499,11 +499,11 @@ def test_register_slab_tracked_flips(golhip, oracle, monkeypatch):
 def test_small_board_picks_register_slab(golhip, oracle):
     """configs[1]-sized boards take the register-slab path automatically (with the planner's own
     depth choice); results unchanged, counts every turn."""
-    # the shape model (pick_reg_kernel): configs[1] 5120^2 keeps 12 x 8 (counting) / 8 x 12 (240
-    # slabs), configs[4] 4096^2 takes 12 x 7 (237 slabs, 21 rows per SIMD)
+    # the shape model (pick_reg_kernel): configs[1] 5120^2 keeps 8 x 12 (240 slabs, 24 rows per
+    # SIMD), configs[4] 4096^2 takes 12 x 7 (237 slabs, 21 rows per SIMD)
     with golhip.Engine(5120, 5120, k=16) as e:
         assert e.launch_kind(16) == ("slab", 20812)
-        assert e.launch_kind(16, counts=True) == ("slab", 21208)
+        assert e.launch_kind(16, counts=True) == ("slab", 20812)
         assert e.launch_kind(8) == ("slab", 808)
         assert e.launch_kind(8, counts=True) == ("slab", 808)
     with golhip.Engine(4096, 4096, k=16) as e:
