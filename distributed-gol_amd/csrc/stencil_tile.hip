@@ -641,7 +641,8 @@ hipError_t launch_slab_kws(const uint32_t *in, uint32_t *out, const StencilParam
 // the tuning neighbours kept measurable (profiles/r03/small_boards_r03.txt)
 #define GOLHIP_SLAB_CONFIGS(X) \
     X(8, 8, 4, 4) X(8, 8, 8, 4) X(12, 8, 8, 4) X(16, 8, 8, 4) X(16, 8, 12, 4) X(16, 16, 8, 4) \
-    X(16, 8, 12, 2) X(16, 12, 8, 2) X(16, 12, 8, 4) X(16, 12, 7, 2) X(16, 10, 8, 2) X(16, 14, 6, 2)
+    X(16, 8, 12, 2) X(16, 12, 8, 2) X(16, 12, 8, 4) X(16, 12, 7, 2) X(16, 10, 8, 2) X(16, 14, 6, 2) \
+    X(16, 16, 6, 2) X(16, 16, 5, 2)
 
 bool stencil_slab_flips_every_gen(int K, int W, int S, int NC) {
     return stencil_slab_supported(K, W, S, NC) && slab_prod_shape(K, W, S, NC);
