@@ -275,7 +275,8 @@ int64_t plan_rows(golhip_t h) { return strip_plan_rows(h->height, h->world_size)
 // Kernel variants whose launches can write a generation's flips beside their output (the
 // production drift family; gol_step1 at K = 1).  The A/B-experiment variants cannot.
 bool variant_writes_flips(int v) {
-    return v == golhip::kVariantProd || v == golhip::kVariantDriftLds || v == golhip::kVariantDrift62;
+    return v == golhip::kVariantProd || v == golhip::kVariantDriftLds || v == golhip::kVariantDrift62 ||
+           v == golhip::kVariantPre63;
 }
 
 int validate_geometry(int width, int height, int world, int k) {
@@ -315,6 +316,7 @@ int setup_engine(golhip_t h, int width, int height, int world, int k) {
                      : std::strcmp(e, "drift62") == 0 ? golhip::kVariantDrift62
                      : std::strcmp(e, "driftnf") == 0 ? golhip::kVariantDriftNoFill
                      : std::strcmp(e, "driftlds") == 0 ? golhip::kVariantDriftLds
+                     : std::strcmp(e, "pre63") == 0 ? golhip::kVariantPre63
                                                        : golhip::kVariantProd;  // prod
     return GOLHIP_OK;
 }

@@ -57,12 +57,15 @@ constexpr int kVariantDriftNoFill = 11;  // driftlds without the compile-time un
 // (profiles/r02/tune_depth_geometry.txt, 65536^2): the half-word halo (63 words, 3 stores per
 // step) at K = 16, 62-word chunks (one store per step) at every other K >= 2; gol_step1 at K = 1.
 constexpr int kVariantProd = 12;
-constexpr int kNumVariants = 13;
+// drift with the input rows pre-shifted K bits west (gol_stencil PRE): 63-word chunks, one whole-word
+// store per step, no store realignment (K <= 16; drift62 above)
+constexpr int kVariantPre63 = 13;
+constexpr int kNumVariants = 14;
 constexpr bool prod_half_halo(int K) { return K == 16; }
 // Variants of the production family: gol_step1 at K = 1, the level-split kernel for small boards.
 inline bool variant_is_production_family(int v) {
     return v == kVariantChainLdsPf || v == kVariantDriftLds || v == kVariantDriftZip ||
-           v == kVariantDrift62 || v == kVariantDriftNoFill || v == kVariantProd;
+           v == kVariantDrift62 || v == kVariantDriftNoFill || v == kVariantProd || v == kVariantPre63;
 }
 inline int variant_words(int v) {
     return (v == kVariantSkewD2 || v == kVariantChainD2 || v == kVariantSkewLdsD2 ||
@@ -79,6 +82,7 @@ inline int chunk_words(int K, int variant) {
     const int d = variant_words(variant);
     if (variant == kVariantDriftZip || variant == kVariantDrift62) return 62;
     if (variant == kVariantProd) return prod_half_halo(K) ? 63 : 62;
+    if (variant == kVariantPre63) return K <= 16 ? 63 : 62;
     return (d == 1 && K <= 16) ? 63 : 62 * d;
 }
 

@@ -290,6 +290,16 @@ __device__ __forceinline__ LaneStore lane_store(int lane, int colraw, int col, i
     return o;
 }
 
+// PRE geometry (gol_stencil PRE): lanes 1..63 own whole words (63 per wave), lane 0 is halo.
+__device__ __forceinline__ LaneStore lane_store_pre(int lane, int colraw, int col, int wd) {
+    LaneStore o;
+    if (lane >= 1 && colraw < wd) {
+        o.off_full = col * 4;
+        o.own_mask = ~0u;
+    }
+    return o;
+}
+
 template <int D, bool HH>
 __device__ __forceinline__ void store_row(__amdgpu_buffer_rsrc_t r, const LaneStore &ls,
                                           const Words<D> &v, int rowoff) {
@@ -357,8 +367,17 @@ __device__ __forceinline__ void flush_counts(const uint32_t (&acc)[NL], int j0, 
 //             store(s) per step.
 // WPE > 0: minimum resident waves per SIMD forced on the register allocator (the vmcnt guard's
 //             self-test instantiates a spilling configuration this way; production: 0).
+// PRE = true (drift, LDS-DMA, K <= 16): the input row is shifted K bits WEST as it leaves the
+//             ring, so the K generations of eastward drift bring the level-K row back to the board
+//             frame: no realignment before the store.  The ring row holds 65 words (the 65th, the
+//             first word of the next chunk, comes from a second DMA of the row one word east), so lane 63's
+//             shifted word is complete, and after K <= 16 generations only lane 0 has gone stale
+//             (2K <= 32 bits from the west edge): 63 whole words per wave with one full-word store
+//             per lane -- the half-word halo's width without its two 16-bit stores.  The shift of
+//             the row and of its west word (2 v_alignbit, the neighbours read from the ring)
+//             replaces the store's realignment (1 DPP + 1 v_alignbit): the same VALU per step.
 template <int K, bool COUNT, bool SKEW, int D, int PF, bool HH, bool DR = false, int ZIP = 1,
-          bool FILLU = true, bool LD = false, int WPE = 0>
+          bool FILLU = true, bool LD = false, int WPE = 0, bool PRE = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     WPE > 0 ? WPE : (ZIP == 2 && !COUNT && K >= 12 && K <= 16 ? 4 : 1))))
 void gol_stencil(const uint32_t *__restrict__ in,
@@ -367,6 +386,8 @@ void gol_stencil(const uint32_t *__restrict__ in,
     static_assert(!HH || (D == 1 && K <= 16), "half-word halo needs D = 1, K <= 16");
     static_assert(!DR || (D == 1 && !SKEW && K <= 32), "drift: one word per lane, chained levels");
     static_assert(ZIP == 1 || (ZIP == 2 && PF == 1 && !SKEW && D == 1), "zip: chained LDS-DMA, D = 1");
+    static_assert(!PRE || (D == 1 && DR && !HH && PF == 1 && ZIP == 1 && K <= 16),
+                  "pre-shifted rows: drift, one word per lane, LDS-DMA ring, K <= 16");
     const int lane = threadIdx.x & 63;
     // wave index made provably uniform so every band/row quantity lives in SGPRs
     const int64_t wave =
@@ -377,7 +398,7 @@ void gol_stencil(const uint32_t *__restrict__ in,
     int ya, yb;
     band_rows(p, bandi, ya, yb);
     // First word (unwrapped) of this lane and its wrapped column.
-    const int stride = HH ? 63 : 62 * D;
+    const int stride = (HH || PRE) ? 63 : 62 * D;
     const int colraw = (int)chunk * stride + (lane - 1) * D;
     const int col = (colraw + p.wd) % p.wd;
     RowStream rows(p, ya - K);
@@ -392,7 +413,7 @@ void gol_stencil(const uint32_t *__restrict__ in,
     const int rowbytes = (int)(p.pitch * 4);
     const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
         out + (int64_t)ya * p.pitch, 0, (yb - ya) * rowbytes, kBufferRsrcWord3);
-    const LaneStore ls = lane_store<HH>(lane, colraw, col, p.wd);
+    const LaneStore ls = PRE ? lane_store_pre(lane, colraw, col, p.wd) : lane_store<HH>(lane, colraw, col, p.wd);
     const uint32_t own_mask = ls.own_mask;
     // DR counts need no per-level mask: level j's row sits d = j+1 bits east, so positions
     // [32, 2048) (lanes 1..63 in full) hold cells [2016c - d, 2016(c+1) - d) of chunk c -- windows
@@ -403,7 +424,11 @@ void gol_stencil(const uint32_t *__restrict__ in,
     // [64, 2048) (lanes 2..63) hold cells [1984c + 32 - d, 1984(c+1) + 32 - d), valid for 2d <= 64;
     // the last chunk's window ends at cell 32 wd + 32 - d, i.e. at the lane with colraw == wd (the
     // wrapped word 0, whose cells [0, 32 - d) no chunk's first window covers).
-    const bool count_lane = HH ? (lane >= 1 && colraw < p.wd) : (lane >= 2 && colraw <= p.wd);
+    // PRE: level j's row sits d = j + 1 - K <= 0 bits east of the board frame, so lanes 1..63 hold
+    // cells [2016c - d, 2016(c+1) - d) (valid: the drift leaves [2(j+1), 2048) valid, 2(j+1) <= 32)
+    // and the lanes with colraw < wd end the last chunk's window at the row end plus -d cells: the
+    // wrapped cells [0, -d) that chunk 0's window leaves out.
+    const bool count_lane = (HH || PRE) ? (lane >= 1 && colraw < p.wd) : (lane >= 2 && colraw <= p.wd);
     // vector-memory stores per step: the output row (3 with the half-word halo), twice with LD
     constexpr int NSTORE = (HH ? 3 : 1) * (LD ? 2 : 1);
     __amdgpu_buffer_rsrc_t drsrc = orsrc;
@@ -484,7 +509,7 @@ void gol_stencil(const uint32_t *__restrict__ in,
             }
             if (j == K - 1) {
                 const int r = st - lag;  // stored row - ya
-                if constexpr (DR) {  // back to the board frame: K bits west
+                if constexpr (DR && !PRE) {  // back to the board frame: K bits west
                     nx.w[0] = realign_drift<K>(nx.w[0]);
                     if constexpr (LD) dv.w[0] = realign_drift<K>(dv.w[0]);
                 }
@@ -585,17 +610,21 @@ void gol_stencil(const uint32_t *__restrict__ in,
         // (D + NSTORE) ops for each of the PL-2 steps after it; the wait leaves a margin of 2.
         // Deeper ring for K <= 2: steps are short, the launch is HBM-bound and needs more bytes
         // in flight per CU.
-        constexpr int PL = (K <= 2 && NSTORE + (D + NSTORE) * 14 - 2 <= 63) ? 16 : 8;
-        constexpr int kWait = NSTORE + (D + NSTORE) * (PL - 2) - 2;
+        // PRE: NDMA = 2 DMAs per row (the row's 64 words and the 65th word)
+        constexpr int NDMA = D + (PRE ? 1 : 0);
+        constexpr int PL = (K <= 2 && NSTORE + (NDMA + NSTORE) * 14 - 2 <= 63) ? 16 : 8;
+        constexpr int kWait = NSTORE + (NDMA + NSTORE) * (PL - 2) - 2;
         static_assert(kWait <= 63, "vmcnt field");
-        __shared__ __attribute__((aligned(16))) uint32_t ring[4][PL][64 * D];
+        __shared__ __attribute__((aligned(16))) uint32_t ring[4][PL][64 * D + (PRE ? 4 : 0)];
         const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
         const int nb_w = max(lane * D - 1, 0), nb_e = min(lane * D + D, 64 * D - 1);
         int dcol4[D];  // byte offset of lane L's word of DMA i in the row
+        int dcol65 = 0;  // PRE: lane L's word of the second DMA (word L + 1 of the ring row)
         {
             const int base = (int)chunk * stride - D;
 #pragma unroll
             for (int i = 0; i < D; ++i) dcol4[i] = ((base + 64 * i + lane + p.wd) % p.wd) * 4;
+            if constexpr (PRE) dcol65 = ((base + 1 + lane + p.wd) % p.wd) * 4;
         }
         // Compiler-level fences (empty asm with a memory clobber) keep every DMA and store in
         // program order, so the per-step vmcnt accounting holds whatever the scheduler does.
@@ -609,6 +638,14 @@ void gol_stencil(const uint32_t *__restrict__ in,
 #pragma unroll
             for (int i = 0; i < D; ++i) {
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, &ring[w][slot][64 * i], 4, dcol4[i], 0, 0, 0);
+                asm volatile("" ::: "memory");
+            }
+            if constexpr (PRE) {
+                // the 65th word: the same row once more, one word east, into ring[1..64] -- lanes
+                // 0..62 rewrite the words the first DMA puts there (same values: the order of the
+                // two LDS writes does not matter), lane 63 adds word 64.  A whole-wave DMA: a
+                // lane-0-only one made the compiler wrap it in exec-mask branches every step
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rr, &ring[w][slot][1], 4, dcol65, 0, 0, 0);
                 asm volatile("" ::: "memory");
             }
             rows.advance();
@@ -674,7 +711,12 @@ void gol_stencil(const uint32_t *__restrict__ in,
                 for (int d = 0; d < D; ++d) vin.w[d] = ring[w][u][lane * D + d];
                 // level 0's neighbour words straight from the ring (the row's lanes -1 / +1; the
                 // edge lanes read a clamped, garbage word: they are halo, as with DPP)
-                const Nb nb0{ring[w][u][nb_w], ring[w][u][nb_e]};
+                Nb nb0{ring[w][u][nb_w], ring[w][u][nb_e]};
+                if constexpr (PRE) {  // the row and its west word, K bits west (lane 63: word 65)
+                    const uint32_t xe = ring[w][u][lane + 1];
+                    nb0.wl = __builtin_amdgcn_alignbit(vin.w[0], nb0.wl, K);
+                    vin.w[0] = __builtin_amdgcn_alignbit(xe, vin.w[0], K);
+                }
                 if (st & 1)
                     step(Par1{}, fill, vin, st, nb0);
                 else
@@ -1028,7 +1070,7 @@ inline const void *step1_fn() {
 }
 
 template <int K, bool SKEW, int D, int PF = 0, bool DR = false, int ZIP = 1, bool HH = kHalfHalo<K, D>,
-          bool FILLU = true, bool ALLOW_LD = false>
+          bool FILLU = true, bool ALLOW_LD = false, bool PRE = false>
 hipError_t launch_stencil_k(const uint32_t *in, uint32_t *out, const StencilParams &p,
                             unsigned long long *slots, hipStream_t s) {
     const int64_t waves = p.nbands * (int64_t)p.nchunks;
@@ -1038,10 +1080,10 @@ hipError_t launch_stencil_k(const uint32_t *in, uint32_t *out, const StencilPara
     if (p.diff) {  // last-generation flips beside the output (production variants only)
         if constexpr (ALLOW_LD) {
             if (slots)
-                hipLaunchKernelGGL((gol_stencil<K, true, SKEW, D, PF, HH, DR, ZIP, FILLU, true>),
+                hipLaunchKernelGGL((gol_stencil<K, true, SKEW, D, PF, HH, DR, ZIP, FILLU, true, 0, PRE>),
                                    dim3(blocks), dim3(256), lds_pad_bytes(), s, in, out, p, slots);
             else
-                hipLaunchKernelGGL((gol_stencil<K, false, SKEW, D, PF, HH, DR, ZIP, FILLU, true>),
+                hipLaunchKernelGGL((gol_stencil<K, false, SKEW, D, PF, HH, DR, ZIP, FILLU, true, 0, PRE>),
                                    dim3(blocks), dim3(256), lds_pad_bytes(), s, in, out, p, slots);
             return hipGetLastError();
         } else {
@@ -1049,10 +1091,10 @@ hipError_t launch_stencil_k(const uint32_t *in, uint32_t *out, const StencilPara
         }
     }
     if (slots)
-        hipLaunchKernelGGL((gol_stencil<K, true, SKEW, D, PF, HH, DR, ZIP, FILLU>), dim3(blocks), dim3(256),
+        hipLaunchKernelGGL((gol_stencil<K, true, SKEW, D, PF, HH, DR, ZIP, FILLU, false, 0, PRE>), dim3(blocks), dim3(256),
                            lds_pad_bytes(), s, in, out, p, slots);
     else
-        hipLaunchKernelGGL((gol_stencil<K, false, SKEW, D, PF, HH, DR, ZIP, FILLU>), dim3(blocks), dim3(256),
+        hipLaunchKernelGGL((gol_stencil<K, false, SKEW, D, PF, HH, DR, ZIP, FILLU, false, 0, PRE>), dim3(blocks), dim3(256),
                            lds_pad_bytes(), s, in, out, p, slots);
     return hipGetLastError();
 }
@@ -1084,6 +1126,10 @@ hipError_t launch_variant(int variant, const uint32_t *in, uint32_t *out, const 
         case kVariantDriftNoFill:
             if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
             else return launch_stencil_k<K, false, 1, 1, (K <= 16), 1, kHalfHalo<K, 1>, false>(in, out, p, slots, s);
+        case kVariantPre63:  // pre-shifted rows, 63-word chunks (K <= 16; drift62 above)
+            if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
+            else if constexpr (K > 16) return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true>(in, out, p, slots, s);
+            else return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true, true>(in, out, p, slots, s);
         case kVariantDriftZip:
             if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
             else return launch_stencil_k<K, false, 1, 1, true, 2, false>(in, out, p, slots, s);
@@ -1116,6 +1162,10 @@ const void *variant_fn(int variant) {
         case kVariantDriftNoFill:
             if constexpr (K == 1) return step1_fn();
             else return (const void *)gol_stencil<K, false, false, 1, 1, kHalfHalo<K, 1>, (K <= 16), 1, false>;
+        case kVariantPre63:
+            if constexpr (K == 1) return step1_fn();
+            else if constexpr (K > 16) return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1>;
+            else return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1, true, false, 0, true>;
         case kVariantDriftZip:
             if constexpr (K == 1) return step1_fn();
             else return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 2>;

@@ -36,8 +36,8 @@ from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
 LLVM = Path(os.environ.get("ROCM_PATH", "/opt/rocm")) / "lib" / "llvm" / "bin"
-STENCIL_ARGS = ["K", "COUNT", "SKEW", "D", "PF", "HH", "DR", "ZIP", "FILLU", "LD", "WPE"]
-DEFAULTS = {"DR": 0, "ZIP": 1, "FILLU": 1, "LD": 0, "WPE": 0}
+STENCIL_ARGS = ["K", "COUNT", "SKEW", "D", "PF", "HH", "DR", "ZIP", "FILLU", "LD", "WPE", "PRE"]
+DEFAULTS = {"DR": 0, "ZIP": 1, "FILLU": 1, "LD": 0, "WPE": 0, "PRE": 0}
 VMEM = re.compile(r"^(buffer_|global_|scratch_|flat_)")
 
 
@@ -102,7 +102,7 @@ def expected_schedule(a: dict[str, int]) -> tuple[int, int, int]:
     """(hand wait immediate, DMAs per row, rows per hand wait) of an LDS-DMA gol_stencil, as
     golhip_stencil.hpp derives them (NSTORE, PL, kWait / kWait2)."""
     nstore = (3 if a["HH"] else 1) * (2 if a["LD"] else 1)
-    d = a["D"]
+    d = a["D"] + a["PRE"]  # PRE: the row's DMA and the single-lane 65th-word DMA
     pl = 16 if (a["K"] <= 2 and nstore + (d + nstore) * 14 - 2 <= 63) else 8
     if a["ZIP"] == 2:
         return 2 * nstore + (2 + 2 * nstore) * (pl // 2 - 2) - 2, d, 2
@@ -113,6 +113,8 @@ def is_production(a: dict[str, int]) -> bool:
     """kVariantProd at depth K (golhip_internal.hpp prod_half_halo / golhip_stencil.hpp):
     drifting sums, one-word lanes, LDS-DMA ring, unrolled fill; half-word halo only at K = 16.
     Any register budget (WPE) counts: the self-test is this kernel forced to spill."""
+    if a["PRE"]:  # the pre-shifted 63-word geometry (kVariantPre63) is held to the same bar
+        return a["SKEW"] == 0 and a["D"] == 1 and a["PF"] == 1 and a["DR"] == 1 and a["ZIP"] == 1
     return (a["SKEW"] == 0 and a["D"] == 1 and a["PF"] == 1 and a["DR"] == 1 and a["ZIP"] == 1
             and a["FILLU"] == 1 and a["HH"] == (1 if a["K"] == 16 else 0))
 
@@ -133,7 +135,13 @@ def linearize(code, hand: set[int]) -> list[int]:
     back edge).  Other branches are ignored: the ring code is branch-free by construction."""
     index = {a: i for i, (a, _, _) in enumerate(code)}
     best = None
-    for i, (a, _, t) in enumerate(code):
+    for i, (a, ins, t) in enumerate(code):
+        # s_cbranch_execz skips a lane-masked region when no lane is active; the ring code's masked
+        # regions (PRE's lane-0 65th-word DMA) always have one, so the branch is never taken -- the
+        # compiler may still close the steady loop with it (rotated loop), which must not be read
+        # as the loop's back edge
+        if ins.startswith("s_cbranch_execz"):
+            continue
         if t is not None and t < a and t in index:
             lo = index[t]
             if any(lo <= h <= i for h in hand) and (best is None or i - lo < best[1] - best[0]):

@@ -90,7 +90,7 @@ def test_flips_match_oracle(golhip, oracle):
             assert [tuple(c) for c in e.flips().tolist()] == oracle.flips(gen_prev, after), n
 
 
-@pytest.mark.parametrize("variant", ["prod", "driftlds", "drift62"])
+@pytest.mark.parametrize("variant", ["prod", "driftlds", "drift62", "pre63"])
 @pytest.mark.parametrize("k", [1, 2, 6, 12, 16, 32])
 @pytest.mark.parametrize("strips", [1, 3])
 def test_tracked_flips_every_depth(golhip, oracle, monkeypatch, variant, k, strips):
@@ -323,7 +323,7 @@ def test_graph_replay_matches_launches(golhip, oracle, monkeypatch, k):
     assert len(cells) == int((exp == 255).sum())
 
 
-@pytest.mark.parametrize("variant", ["chainlds", "driftlds", "driftzip", "drift62", "driftnf", "skewlds", "chainlds2",
+@pytest.mark.parametrize("variant", ["chainlds", "driftlds", "driftzip", "drift62", "driftnf", "pre63", "skewlds", "chainlds2",
                                      "skewlds2", "chain", "skew", "chain2", "skew2"])
 @pytest.mark.parametrize("k", [1, 6, 16])
 def test_every_kernel_variant(golhip, oracle, monkeypatch, variant, k):
@@ -341,12 +341,13 @@ def test_every_kernel_variant(golhip, oracle, monkeypatch, variant, k):
             assert np.array_equal(counts.astype(np.int64), exp_counts), (variant, k, h, w, band)
 
 
-@pytest.mark.parametrize("variant", ["driftlds", "driftzip", "drift62"])
+@pytest.mark.parametrize("variant", ["driftlds", "driftzip", "drift62", "pre63"])
 @pytest.mark.parametrize("k", [2, 4, 6, 8, 10, 12, 14, 16, 32])
 def test_drift_variant_every_k(golhip, oracle, monkeypatch, variant, k):
     """The drifting-sum stencils (rows move one bit east per level, one DPP per level update) --
-    half-word-halo chunks (driftlds), 62-word chunks (drift62) and 62-word chunks with two steps
-    interleaved (driftzip): every launch depth, per-turn counts (drifted count windows), multi-
+    half-word-halo chunks (driftlds), 62-word chunks (drift62), 62-word chunks with two steps
+    interleaved (driftzip) and 63-word chunks of rows pre-shifted K bits west (pre63, its 65th-word
+    DMA and no store realignment): every launch depth, per-turn counts (drifted count windows), multi-
     chunk rows with a partial last chunk and widths that are not a multiple of 128 (replicated
     torus)."""
     monkeypatch.setenv("GOLHIP_VARIANT", variant)
