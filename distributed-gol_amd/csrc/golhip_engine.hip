@@ -93,6 +93,7 @@ struct golhip_engine {
     int32_t wd = 0;
     int world_size = 1;
     int k = 1, halo = 0, band_rows = 0;
+    int tail_bands = 0, tail_rows = 0;  // golhip_set_tail_bands: graded bands (0 = uniform)
     int count_window = 4096;  // generations per count-window finalize
     int variant = golhip::kVariantProd;  // fastest measured per depth (golhip_internal.hpp)
     int cus = 0;                 // compute units of the first device (grid sizing)
@@ -601,6 +602,7 @@ hipError_t launch_auto(golhip_t h, int K, const uint32_t *in, uint32_t *out,
         StencilParams q = p;
         const int T = rk.out_rows();
         q.band = T;
+        q.band2 = q.nbig0 = 0;
         q.nbands0 = (p.r0e - p.r0b + T - 1) / T;
         q.nbands = q.nbands0 + (p.r1e - p.r1b + T - 1) / T;
         q.nchunks = (int32_t)((h->wd + golhip::kTileChunkWords - 1) / golhip::kTileChunkWords);
@@ -611,6 +613,11 @@ hipError_t launch_auto(golhip_t h, int K, const uint32_t *in, uint32_t *out,
     if (S > 1) {
         // the level-split kernel has its own column geometry (half-word halo for K <= 16)
         StencilParams q = p;
+        if (q.band2 > 0) {  // uniform bands for the level-split kernel
+            q.band2 = q.nbig0 = 0;
+            q.nbands0 = (p.r0e - p.r0b + p.band - 1) / p.band;
+            q.nbands = q.nbands0 + (p.r1e - p.r1b + p.band - 1) / p.band;
+        }
         const int per = golhip::split_chunk_words(K);
         q.nchunks = (int32_t)((h->wd + per - 1) / per);
         return golhip::launch_stencil_split(K, S, in, out, q, slots, s);
@@ -629,6 +636,13 @@ StencilParams make_params(golhip_t h, const Shard &s, int K, int64_t r0b, int64_
     const int64_t total = (r0e - r0b) + (r1e - r1b);
     p.band = std::min(auto_band(h, std::max<int64_t>(total, 1), K, reserve_waves), max_band_rows(h));
     p.nbands0 = (r0e - r0b + p.band - 1) / p.band;
+    // graded bands (golhip_set_tail_bands): range 0 ends in tail_bands bands of tail_rows rows
+    const int64_t n2 = h->tail_bands, b2 = h->tail_rows, R0 = r0e - r0b;
+    if (n2 > 0 && b2 > 0 && b2 < p.band && R0 > n2 * b2) {
+        p.nbig0 = (R0 - n2 * b2) / p.band;
+        p.band2 = b2;
+        p.nbands0 = p.nbig0 + (R0 - p.nbig0 * p.band + b2 - 1) / b2;
+    }
     p.nbands = p.nbands0 + (r1e - r1b + p.band - 1) / p.band;
     p.wrap_rows = h->split ? 0 : h->height;
     p.lo = -(int64_t)h->halo;
@@ -1881,6 +1895,13 @@ int golhip_set_fixed_k(golhip_t h, int fixed) {
 int golhip_set_band_rows(golhip_t h, int band_rows) {
     if (!h || band_rows < 0) return GOLHIP_ERR_ARG;
     h->band_rows = band_rows;
+    return GOLHIP_OK;
+}
+
+int golhip_set_tail_bands(golhip_t h, int bands, int rows) {
+    if (!h || bands < 0 || rows < 0) return GOLHIP_ERR_ARG;
+    h->tail_bands = bands;
+    h->tail_rows = rows;
     return GOLHIP_OK;
 }
 

@@ -21,6 +21,9 @@ struct StencilParams {
     int64_t r0b, r0e;    // output range 0
     int64_t r1b, r1e;    // output range 1 (r1b == r1e: none)
     int64_t band;        // output rows per wave band
+    // > 0: range 0 is nbig0 bands of `band` rows, then bands of band2 rows (shorter: the last
+    // dispatched waves are short, so the launch's tail is short -- graded bands)
+    int64_t band2, nbig0;
     int64_t nbands0;     // bands in range 0
     int64_t nbands;      // bands in total
     int64_t wrap_rows;   // > 0: single strip holding the whole torus height (row index mod H)
@@ -53,15 +56,17 @@ constexpr int kVariantDriftLds = 8;    // chained LDS-DMA levels with drifting r
 constexpr int kVariantDriftZip = 9;    // drift, 62-word chunks, two steps interleaved (ZIP = 2)
 constexpr int kVariantDrift62 = 10;    // drift, 62-word chunks (one whole-word store per step)
 constexpr int kVariantDriftNoFill = 11;  // driftlds without the compile-time unrolled fill
-// Production: drifting sums at every depth, with the chunk geometry measured fastest per depth
-// (profiles/r02/tune_depth_geometry.txt, 65536^2): the half-word halo (63 words, 3 stores per
-// step) at K = 16, 62-word chunks (one store per step) at every other K >= 2; gol_step1 at K = 1.
+// Production: drifting sums at every depth, with the chunk geometry measured fastest per depth:
+// at K = 16 the pre-shifted 63-word rows (PRE, below; round 3: +2.9 % at 65536^2 and +3.0 % at
+// 262144^2 over the half-word halo, pre-heated lockstep A/B, profiles/r03/r03p_ab_*.log), 62-word
+// chunks (one store per step) at every other K >= 2 (PRE measured equal at K = 12, +0.6 % at 8;
+// profiles/r02/tune_depth_geometry.txt for the earlier geometries); gol_step1 at K = 1.
 constexpr int kVariantProd = 12;
 // drift with the input rows pre-shifted K bits west (gol_stencil PRE): 63-word chunks, one whole-word
 // store per step, no store realignment (K <= 16; drift62 above)
 constexpr int kVariantPre63 = 13;
 constexpr int kNumVariants = 14;
-constexpr bool prod_half_halo(int K) { return K == 16; }
+constexpr bool prod_pre(int K) { return K == 16; }
 // Variants of the production family: gol_step1 at K = 1, the level-split kernel for small boards.
 inline bool variant_is_production_family(int v) {
     return v == kVariantChainLdsPf || v == kVariantDriftLds || v == kVariantDriftZip ||
@@ -81,7 +86,7 @@ inline int chunk_words(int K, int variant) {
         return 256;  // gol_step1: 4 words x 64 lanes
     const int d = variant_words(variant);
     if (variant == kVariantDriftZip || variant == kVariantDrift62) return 62;
-    if (variant == kVariantProd) return prod_half_halo(K) ? 63 : 62;
+    if (variant == kVariantProd) return prod_pre(K) ? 63 : 62;
     if (variant == kVariantPre63) return K <= 16 ? 63 : 62;
     return (d == 1 && K <= 16) ? 63 : 62 * d;
 }

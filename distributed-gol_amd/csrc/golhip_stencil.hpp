@@ -230,8 +230,13 @@ __device__ __forceinline__ void level_ingest(RowState<D> &above, const Words<D> 
 // SALU (gfx9 has no 64-bit signed s_cmp, a 64-bit compare would drag them into VGPRs).
 __device__ __forceinline__ void band_rows(const StencilParams &p, int64_t bandi, int &ya, int &yb) {
     if (bandi < p.nbands0) {
-        ya = (int)(p.r0b + bandi * p.band);
-        yb = (int)min((int64_t)ya + p.band, p.r0e);
+        if (p.band2 > 0 && bandi >= p.nbig0) {  // graded: the short tail bands
+            ya = (int)(p.r0b + p.nbig0 * p.band + (bandi - p.nbig0) * p.band2);
+            yb = (int)min((int64_t)ya + p.band2, p.r0e);
+        } else {
+            ya = (int)(p.r0b + bandi * p.band);
+            yb = (int)min((int64_t)ya + p.band, p.r0e);
+        }
     } else {
         ya = (int)(p.r1b + (bandi - p.nbands0) * p.band);
         yb = (int)min((int64_t)ya + p.band, p.r1e);
@@ -378,8 +383,11 @@ __device__ __forceinline__ void flush_counts(const uint32_t (&acc)[NL], int j0, 
 //             replaces the store's realignment (1 DPP + 1 v_alignbit): the same VALU per step.
 template <int K, bool COUNT, bool SKEW, int D, int PF, bool HH, bool DR = false, int ZIP = 1,
           bool FILLU = true, bool LD = false, int WPE = 0, bool PRE = false>
+// (PRE with counts at K = 16 (production): left alone, the allocator spends 224 VGPRs, i.e. 2 waves
+// per SIMD; held to the half-word-halo kernel's 3 it needs 142 and no scratch.  At K = 12, 4 waves
+// would spill: no hint there.)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
-    WPE > 0 ? WPE : (ZIP == 2 && !COUNT && K >= 12 && K <= 16 ? 4 : 1))))
+    WPE > 0 ? WPE : (ZIP == 2 && !COUNT && K >= 12 && K <= 16 ? 4 : (PRE && COUNT && K >= 14 ? 3 : 1)))))
 void gol_stencil(const uint32_t *__restrict__ in,
                                                    uint32_t *__restrict__ out, StencilParams p,
                                                    unsigned long long *__restrict__ slots) {
@@ -1121,7 +1129,7 @@ hipError_t launch_variant(int variant, const uint32_t *in, uint32_t *out, const 
             else return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true>(in, out, p, slots, s);
         case kVariantProd:  // per depth: the fastest measured (golhip_internal.hpp)
             if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
-            else if constexpr (prod_half_halo(K)) return launch_stencil_k<K, false, 1, 1, true, 1, true, true, true>(in, out, p, slots, s);
+            else if constexpr (prod_pre(K)) return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true, true>(in, out, p, slots, s);
             else return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true>(in, out, p, slots, s);
         case kVariantDriftNoFill:
             if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
@@ -1157,7 +1165,7 @@ const void *variant_fn(int variant) {
             else return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1>;
         case kVariantProd:
             if constexpr (K == 1) return step1_fn();
-            else if constexpr (prod_half_halo(K)) return (const void *)gol_stencil<K, false, false, 1, 1, true, true, 1>;
+            else if constexpr (prod_pre(K)) return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1, true, false, 0, true>;
             else return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1>;
         case kVariantDriftNoFill:
             if constexpr (K == 1) return step1_fn();

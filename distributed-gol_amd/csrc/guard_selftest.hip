@@ -9,7 +9,7 @@ namespace golhip {
 
 hipError_t guard_selftest_launch(const uint32_t *in, uint32_t *out, const StencilParams &p,
                                  hipStream_t s) {
-    hipLaunchKernelGGL((gol_stencil<16, false, false, 1, 1, true, true, 1, true, false, 8>),
+    hipLaunchKernelGGL((gol_stencil<16, false, false, 1, 1, false, true, 1, true, false, 8, true>),
                        dim3(1), dim3(256), 0, s, in, out, p, nullptr);
     return hipGetLastError();
 }

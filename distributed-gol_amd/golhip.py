@@ -39,7 +39,7 @@ EXPORTS = [
     "golhip_last_error", "golhip_get_info", "golhip_load_bytes", "golhip_init_random",
     "golhip_store_bytes", "golhip_store_words", "golhip_load_words", "golhip_step",
     "golhip_alive_count", "golhip_alive_cells", "golhip_flips", "golhip_turn",
-    "golhip_set_turn", "golhip_set_k", "golhip_set_band_rows", "golhip_sync", "golhip_timing",
+    "golhip_set_turn", "golhip_set_k", "golhip_set_band_rows", "golhip_set_tail_bands", "golhip_sync", "golhip_timing",
     "golhip_kernel_time", "golhip_launch_plan", "golhip_launch_kind", "golhip_launch_kind_counts", "golhip_set_fixed_k", "golhip_track_flips",
     "golhip_step_flips", "golhip_flips_ring_capacity", "golhip_flips_fetch",
     "golhip_checkpoint_save", "golhip_checkpoint_load", "golhip_checkpoint_info",
@@ -168,6 +168,7 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
         "golhip_set_turn": ([H, i64], i32),
         "golhip_set_k": ([H, i32], i32),
         "golhip_set_band_rows": ([H, i32], i32),
+        "golhip_set_tail_bands": ([H, i32, i32], i32),
         "golhip_set_fixed_k": ([H, i32], i32),
         "golhip_track_flips": ([H, i32], i32),
         "golhip_checkpoint_save": ([H, ctypes.c_char_p], i32),
@@ -471,6 +472,9 @@ class Engine:
 
     def set_band_rows(self, rows: int):
         self._check(self._L.golhip_set_band_rows(self._h, rows))
+
+    def set_tail_bands(self, bands: int, rows: int):
+        self._check(self._L.golhip_set_tail_bands(self._h, bands, rows))
         self.info = self.get_info()
 
     def launch_kind(self, k: int, counts: bool = False) -> tuple[str, int]:

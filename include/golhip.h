@@ -203,6 +203,9 @@ int golhip_set_k(golhip_t h, int k);                 /* 1..32, <= halo_rows when
  * (golhip_launch_plan).  fixed != 0: every bulk launch is exactly k deep (depth sweeps). */
 int golhip_set_fixed_k(golhip_t h, int fixed);
 int golhip_set_band_rows(golhip_t h, int band_rows); /* 0 = automatic */
+/* Graded bands (tuning): the streaming launch's rows end in `bands` bands of `rows` rows each
+ * instead of full-height ones (0, 0 = uniform bands). */
+int golhip_set_tail_bands(golhip_t h, int bands, int rows);
 /* Which kernel a k-deep launch on this handle's first strip runs: *kind = 0 the streaming kernel
  * (gol_stencil, gol_step1 at k = 1), 1 the level-split kernel (*param = waves per band), 2 the
  * register-tile kernel gol_tile (*param = tile height T), 3 the register-slab kernel gol_slab

@@ -110,13 +110,12 @@ def expected_schedule(a: dict[str, int]) -> tuple[int, int, int]:
 
 
 def is_production(a: dict[str, int]) -> bool:
-    """kVariantProd at depth K (golhip_internal.hpp prod_half_halo / golhip_stencil.hpp):
-    drifting sums, one-word lanes, LDS-DMA ring, unrolled fill; half-word halo only at K = 16.
-    Any register budget (WPE) counts: the self-test is this kernel forced to spill."""
-    if a["PRE"]:  # the pre-shifted 63-word geometry (kVariantPre63) is held to the same bar
-        return a["SKEW"] == 0 and a["D"] == 1 and a["PF"] == 1 and a["DR"] == 1 and a["ZIP"] == 1
+    """kVariantProd at depth K (golhip_internal.hpp prod_pre / golhip_stencil.hpp): drifting sums,
+    one-word lanes, LDS-DMA ring, unrolled fill, whole-word chunks; pre-shifted rows (PRE) at
+    K = 16.  The pre-shifted geometry at other depths (kVariantPre63) is held to the same bar.
+    Any register budget (WPE) counts: the self-test is the K = 16 kernel forced to spill."""
     return (a["SKEW"] == 0 and a["D"] == 1 and a["PF"] == 1 and a["DR"] == 1 and a["ZIP"] == 1
-            and a["FILLU"] == 1 and a["HH"] == (1 if a["K"] == 16 else 0))
+            and a["FILLU"] == 1 and a["HH"] == 0 and (a["PRE"] == 1 or a["K"] != 16))
 
 
 def is_dma(ins: str) -> bool:

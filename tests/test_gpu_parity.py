@@ -363,6 +363,27 @@ def test_drift_variant_every_k(golhip, oracle, monkeypatch, variant, k):
             assert count == int((exp == 255).sum())
 
 
+@pytest.mark.parametrize("k", [1, 2, 8, 12, 16])
+def test_graded_tail_bands(golhip, oracle, k):
+    """Graded bands (golhip_set_tail_bands): range 0 ends in short bands after the full-height
+    ones -- band seams at both heights, a partial last tail band, a tail longer than the rows
+    (ignored), on the streaming kernels (explicit band height) with per-turn counts."""
+    for (h, w) in [(300, 4160), (131, 2016), (77, 640)]:
+        rng = np.random.default_rng(h * 13 + w + k)
+        board = ((rng.random((h, w)) < 0.41) * 255).astype(np.uint8)
+        turns = 2 * k + 3
+        exp, exp_counts = oracle.packed_run(board, turns)
+        for band, tail in [(40, (3, 9)), (64, (5, 13)), (24, (1, 8)), (40, (100, 20))]:
+            with golhip.Engine(w, h, k=k) as e:
+                e.set_fixed_k(True)
+                e.set_band_rows(band)
+                e.set_tail_bands(*tail)
+                e.load(board)
+                c = e.step(turns, counts=True)
+                assert np.array_equal(e.store(), exp), (k, h, w, band, tail)
+                assert np.array_equal(c.astype(np.int64), exp_counts), (k, h, w, band, tail)
+
+
 @pytest.mark.parametrize("split,k", [(s, k) for k in (4, 6, 8, 16, 32) for s in (2, 4, 8)
                                      if k % s == 0])  # levels split evenly over the waves
 def test_level_split_kernel(golhip, oracle, monkeypatch, split, k):

@@ -13,10 +13,11 @@ sys.path.insert(0, str(ROOT / "scripts"))
 import check_vmcnt as cv  # noqa: E402
 
 
-def ring_kernel(K=16, HH=1, LD=0, D=1, nstore=None, wait=None, steady_steps=8):
+def ring_kernel(K=16, HH=1, LD=0, D=1, nstore=None, wait=None, steady_steps=8, PRE=0):
     """A synthetic LDS-DMA stencil as the disassembler shows it: PL-1 prologue rows (DMA +
-    dummy stores), 2K fill steps, a PL-step steady loop with a back edge, then the drain."""
-    args = dict(K=K, COUNT=0, SKEW=0, D=D, PF=1, HH=HH, DR=1, ZIP=1, FILLU=1, LD=LD, WPE=0)
+    dummy stores), 2K fill steps, a PL-step steady loop with a back edge, then the drain.
+    PRE: two DMAs per row (the row and the row one word east)."""
+    args = dict(K=K, COUNT=0, SKEW=0, D=D, PF=1, HH=HH, DR=1, ZIP=1, FILLU=1, LD=LD, WPE=0, PRE=PRE)
     w, dmas, _ = cv.expected_schedule(args)
     ns = nstore if nstore is not None else (3 if HH else 1) * (2 if LD else 1)
     code, addr = [], 0x1000
@@ -27,7 +28,7 @@ def ring_kernel(K=16, HH=1, LD=0, D=1, nstore=None, wait=None, steady_steps=8):
         addr += 8
 
     def row():
-        for _ in range(D):
+        for _ in range(D + PRE):
             emit("buffer_load_dword v3, s[0:3], 0 offen lds")
 
     def stores():
@@ -42,13 +43,14 @@ def ring_kernel(K=16, HH=1, LD=0, D=1, nstore=None, wait=None, steady_steps=8):
         emit("v_bitop3_b32 v9, v10, v11, v12 bitop3:0x96")
         stores()
 
-    for _ in range(7):
+    pl = 16 if (K <= 2 and ns + (dmas + ns) * 14 - 2 <= 63) else 8  # the kernel's ring depth
+    for _ in range(pl - 1):
         row()
         stores()
-    for _ in range(2 * K):
+    for _ in range((2 * K + pl - 1) // pl * pl):
         step()
     top = addr
-    for _ in range(steady_steps):
+    for _ in range(max(steady_steps, pl)):
         step()
     emit("s_cmp_lt_i32 s4, s5")
     emit("s_cbranch_scc1 65000", top)
@@ -57,9 +59,30 @@ def ring_kernel(K=16, HH=1, LD=0, D=1, nstore=None, wait=None, steady_steps=8):
     return code, (w, dmas, 1)
 
 
-@pytest.mark.parametrize("K,HH,LD", [(16, 1, 0), (16, 1, 1), (8, 0, 0), (12, 0, 1)])
-def test_correct_schedule_passes(K, HH, LD):
-    code, sched = ring_kernel(K=K, HH=HH, LD=LD)
+@pytest.mark.parametrize("K,HH,LD,PRE", [(16, 1, 0, 0), (16, 1, 1, 0), (8, 0, 0, 0), (12, 0, 1, 0),
+                                         (16, 0, 0, 1), (16, 0, 1, 1), (2, 0, 0, 1)])
+def test_correct_schedule_passes(K, HH, LD, PRE):
+    code, sched = ring_kernel(K=K, HH=HH, LD=LD, PRE=PRE)
+    assert cv.simulate(code, *sched, split=False) == []
+
+
+def test_pre_wait_without_its_second_dma_fails():
+    # a pre-shifted kernel whose hand wait counts two DMAs per row while the code issues one (the
+    # second DMA merged away or hoisted out of the step): the wait is too loose for its row
+    _, (w_pre, d_pre, _) = ring_kernel(K=16, HH=0, PRE=1)
+    assert d_pre == 2
+    code, (w, d, z) = ring_kernel(K=16, HH=0, PRE=0, wait=w_pre)
+    assert w_pre > w and d == 1
+    assert cv.simulate(code, w_pre, d, z, split=False)
+
+
+def test_masked_region_skip_is_not_a_back_edge():
+    # a lane-masked region at the end of the steady loop, closed by an execz skip to the loop top
+    # (what the compiler emitted for a lane-0-only DMA): the model follows the fall-through path
+    code, sched = ring_kernel(K=8, HH=0)
+    top = next(a for a, ins, _ in code if ins.startswith("s_waitcnt vmcnt(") and ins != "s_waitcnt vmcnt(0)")
+    i = next(i for i, c in enumerate(code) if c[1].startswith("s_cbranch_scc1"))
+    code.insert(i, (code[i][0] - 4, "s_cbranch_execz 65000", top))
     assert cv.simulate(code, *sched, split=False) == []
 
 
@@ -95,20 +118,25 @@ def test_missing_hand_wait_fails():
 
 
 def test_production_classification():
-    base = dict(COUNT=0, SKEW=0, D=1, PF=1, DR=1, ZIP=1, FILLU=1, LD=0, WPE=0)
-    assert cv.is_production(dict(base, K=16, HH=1))
+    base = dict(COUNT=0, SKEW=0, D=1, PF=1, DR=1, ZIP=1, FILLU=1, LD=0, WPE=0, PRE=0)
+    assert cv.is_production(dict(base, K=16, HH=0, PRE=1))
     assert cv.is_production(dict(base, K=8, HH=0, LD=1))
-    assert not cv.is_production(dict(base, K=16, HH=0))       # drift62 at K = 16: experiment
-    assert cv.is_production(dict(base, K=16, HH=1, WPE=8))  # the self-test: production, spilling
+    assert cv.is_production(dict(base, K=12, HH=0, PRE=1))     # pre63 at K = 12: same bar
+    assert not cv.is_production(dict(base, K=16, HH=0))        # drift62 at K = 16: experiment
+    assert not cv.is_production(dict(base, K=16, HH=1))        # half-word halo: superseded
+    assert cv.is_production(dict(base, K=16, HH=0, PRE=1, WPE=8))  # the self-test: production, spilling
     assert not cv.is_production(dict(base, K=8, HH=0, ZIP=2))
 
 
 def test_mangled_template_arguments():
-    name = ("_ZN6golhip12_GLOBAL__N_111gol_stencilILi16ELb0ELb0ELi1ELi1ELb1ELb1ELi1ELb1ELb0ELi0EEEvPKjPjNS_"
+    name = ("_ZN6golhip12_GLOBAL__N_111gol_stencilILi16ELb0ELb0ELi1ELi1ELb0ELb1ELi1ELb1ELb0ELi0ELb1EEEvPKjPjNS_"
             "13StencilParamsEPy")
     a = cv.stencil_args(name)
-    assert (a["K"], a["HH"], a["DR"], a["LD"], a["WPE"]) == (16, 1, 1, 0, 0)
+    assert (a["K"], a["HH"], a["DR"], a["LD"], a["WPE"], a["PRE"]) == (16, 0, 1, 0, 0, 1)
     assert cv.is_production(a)
+    old = ("_ZN6golhip12_GLOBAL__N_111gol_stencilILi16ELb0ELb0ELi1ELi1ELb1ELb1ELi1ELb1ELb0ELi0EEEvPKjPjNS_"
+           "13StencilParamsEPy")  # a name without the trailing PRE argument: PRE defaults to 0
+    assert cv.stencil_args(old)["PRE"] == 0
 
 
 needs_objs = pytest.mark.skipif(not (LIB / "guard_selftest.o").exists() or not (LIB / "stencil_k16.o").exists(),
