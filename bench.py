@@ -583,13 +583,23 @@ def main():
             cap = fe.flips_ring_capacity()
             T = min(cap, 128)
             fe.step_flips(T)  # allocate the ring, warm
+            fe.step_flips_rows(T)
             reps = max(1, 2048 // T)
             cells = 0
+            fe.init_random(7)  # both forms time the same turns of the same board
             t0 = time.perf_counter()
             for _ in range(reps):
                 per_turn, _ = fe.step_flips(T)
                 cells += sum(len(x) for x in per_turn)
             dt = time.perf_counter() - t0
+            # the compact form (golhip_step_flips_rows: uint16 x + per-turn-row offsets)
+            fe.init_random(7)
+            cells_r = 0
+            t2 = time.perf_counter()
+            for _ in range(reps):
+                x, _, _ = fe.step_flips_rows(T)
+                cells_r += len(x)
+            dt2 = time.perf_counter() - t2
             t1 = time.perf_counter()
             for _ in range(64):
                 fe.step(1)
@@ -598,6 +608,8 @@ def main():
             fe.close()
             flips[f"{n}x{n}"] = {"us_per_turn": round(dt / (reps * T) * 1e6, 2),
                                  "turns_per_call": T, "flips_per_turn": round(cells / (reps * T), 1),
+                                 "us_per_turn_rows": round(dt2 / (reps * T) * 1e6, 2),
+                                 "rows_same_cells": cells_r == cells,
                                  "us_per_turn_step1_then_flips": round(dt1 / 64 * 1e6, 2)}
 
     small = None

@@ -1549,16 +1549,9 @@ int golhip_flips_ring_capacity(golhip_t h, int64_t *out) {
     return GOLHIP_OK;
 }
 
-int golhip_step_flips(golhip_t h, int64_t turns, int32_t *xy, size_t cap, size_t *n,
-                      uint64_t *flips_per_turn, uint64_t *alive_per_turn) {
-    if (!h || turns < 0 || !n) return GOLHIP_ERR_ARG;
-    const int64_t rc_cap = ring_capacity(h);
-    if (turns > rc_cap)
-        return fail(h, GOLHIP_ERR_ARG, "%lld turns exceed the flips ring (%lld turns)",
-                    (long long)turns, (long long)rc_cap);
-    *n = 0;
-    if (turns == 0) return GOLHIP_OK;
-    if (h->ring_cap < rc_cap) {  // allocate the ring once per engine
+// The per-turn flips ring: allocated once per engine (ring_capacity turns of strip-sized slots).
+static int ensure_ring(golhip_t h, int64_t rc_cap) {
+    if (h->ring_cap < rc_cap) {
         for (auto &s : h->shards) {
             HIPCHK(h, hipSetDevice(s.device));
             HIPCHK(h, hipStreamSynchronize(s.compute));
@@ -1570,7 +1563,21 @@ int golhip_step_flips(golhip_t h, int64_t turns, int32_t *xy, size_t cap, size_t
         }
         h->ring_cap = rc_cap;
     }
-    int rc = run_steps(h, turns, alive_per_turn, true);
+    return GOLHIP_OK;
+}
+
+int golhip_step_flips(golhip_t h, int64_t turns, int32_t *xy, size_t cap, size_t *n,
+                      uint64_t *flips_per_turn, uint64_t *alive_per_turn) {
+    if (!h || turns < 0 || !n) return GOLHIP_ERR_ARG;
+    const int64_t rc_cap = ring_capacity(h);
+    if (turns > rc_cap)
+        return fail(h, GOLHIP_ERR_ARG, "%lld turns exceed the flips ring (%lld turns)",
+                    (long long)turns, (long long)rc_cap);
+    *n = 0;
+    if (turns == 0) return GOLHIP_OK;
+    int rc = ensure_ring(h, rc_cap);
+    if (rc) return rc;
+    rc = run_steps(h, turns, alive_per_turn, true);
     if (rc) return rc;
     h->ring_turns = turns;
     std::vector<const uint32_t *> a, b(h->shards.size(), nullptr);
@@ -1587,6 +1594,81 @@ int golhip_flips_fetch(golhip_t h, int32_t *xy, size_t cap, size_t *n, uint64_t 
     std::vector<const uint32_t *> a, b(h->shards.size(), nullptr);
     for (auto &s : h->shards) a.push_back(s.ring);
     return extract_cells(h, a, b, h->ring_turns, xy, cap, n, flips_per_turn);
+}
+
+// The flips ring as x-only rows (golhip_step_flips_rows / golhip_flips_fetch_rows): one strip
+// per handle, width <= 65536.  row_offsets (slots * rows + 1 entries) = the exclusive scan of the
+// ring's row counts, copied straight from the extraction scan; x = the cells' x as uint16 in the
+// same order: 2 bytes per flip instead of the 8 of an (x, y) pair.
+int extract_rows(golhip_t h, int64_t slots, uint16_t *x, size_t cap, size_t *n,
+                 uint64_t *row_offsets) {
+    Shard &s = h->shards[0];
+    const int64_t rows = s.rows * slots;
+    int rc = ensure_extract_scratch(h, s, rows, slots);
+    if (rc) return rc;
+    HIPCHK(h, hipSetDevice(s.device));
+    HIPCHK(h, golhip::launch_extract_count(s.ring, nullptr, h->pitch, rows, h->width, s.ex_rowcounts,
+                                           s.ex_offsets, s.ex_block_sums, s.compute));
+    HIPCHK(h, hipMemcpyAsync(row_offsets, s.ex_offsets, sizeof(uint64_t) * (size_t)(rows + 1),
+                             hipMemcpyDeviceToHost, s.compute));
+    HIPCHK(h, hipStreamSynchronize(s.compute));
+    const size_t total = (size_t)row_offsets[rows];
+    *n = total;
+    if (total > cap) return fail(h, GOLHIP_ERR_CAP, "%zu cells do not fit in cap %zu", total, cap);
+    if (total == 0) return GOLHIP_OK;
+    if (!x) return fail(h, GOLHIP_ERR_ARG, "x is null");
+    if (total > s.ex_xy_cap) {  // the (x, y) list's device buffer holds 4x as many x-only cells
+        if (s.ex_xy) HIPCHK(h, hipFree(s.ex_xy));
+        s.ex_xy = nullptr;
+        const size_t want = std::max(total, s.ex_xy_cap * 2);
+        HIPCHK(h, hipMalloc(&s.ex_xy, sizeof(int32_t) * 2 * want));
+        s.ex_xy_cap = want;
+    }
+    uint16_t *dx = reinterpret_cast<uint16_t *>(s.ex_xy);
+    HIPCHK(h, golhip::launch_extract_emit_x16(s.ring, nullptr, h->pitch, rows, h->width, s.ex_offsets,
+                                              dx, total, s.compute));
+    HIPCHK(h, hipMemcpyAsync(x, dx, sizeof(uint16_t) * total, hipMemcpyDeviceToHost, s.compute));
+    HIPCHK(h, hipStreamSynchronize(s.compute));
+    return GOLHIP_OK;
+}
+
+static int rows_api_check(golhip_t h, uint64_t *row_offsets, size_t *n) {
+    if (!h || !n || !row_offsets) return GOLHIP_ERR_ARG;
+    if (h->shards.size() != 1)
+        return fail(h, GOLHIP_ERR_STATE, "flips rows: one strip per handle (%zu here)", h->shards.size());
+    if (h->width > 65536)
+        return fail(h, GOLHIP_ERR_ARG, "flips rows: x is uint16, width %lld > 65536", (long long)h->width);
+    return GOLHIP_OK;
+}
+
+int golhip_step_flips_rows(golhip_t h, int64_t turns, uint16_t *x, size_t cap, size_t *n,
+                           uint64_t *row_offsets, uint64_t *alive_per_turn) {
+    int rc = rows_api_check(h, row_offsets, n);
+    if (rc) return rc;
+    if (turns < 0) return GOLHIP_ERR_ARG;
+    const int64_t rc_cap = ring_capacity(h);
+    if (turns > rc_cap)
+        return fail(h, GOLHIP_ERR_ARG, "%lld turns exceed the flips ring (%lld turns)",
+                    (long long)turns, (long long)rc_cap);
+    *n = 0;
+    row_offsets[0] = 0;
+    if (turns == 0) return GOLHIP_OK;
+    rc = ensure_ring(h, rc_cap);
+    if (rc) return rc;
+    rc = run_steps(h, turns, alive_per_turn, true);
+    if (rc) return rc;
+    h->ring_turns = turns;
+    return extract_rows(h, turns, x, cap, n, row_offsets);
+}
+
+int golhip_flips_fetch_rows(golhip_t h, uint16_t *x, size_t cap, size_t *n, uint64_t *row_offsets) {
+    int rc = rows_api_check(h, row_offsets, n);
+    if (rc) return rc;
+    if (h->ring_turns == 0)
+        return fail(h, GOLHIP_ERR_STATE, "no golhip_step_flips call holds flips in the ring");
+    rc = sync_all(h);
+    if (rc) return rc;
+    return extract_rows(h, h->ring_turns, x, cap, n, row_offsets);
 }
 
 int golhip_track_flips(golhip_t h, int enable) {

@@ -179,6 +179,10 @@ hipError_t launch_extract_emit(const uint32_t *a, const uint32_t *b, int64_t pit
                                int64_t rows, int64_t width, const unsigned long long *offsets,
                                int64_t gy0, int64_t slot_rows, int32_t *xy, uint64_t cap,
                                hipStream_t s);
+// x coordinates only, as uint16 (width <= 65536), in the same order (golhip_step_flips_rows).
+hipError_t launch_extract_emit_x16(const uint32_t *a, const uint32_t *b, int64_t pitch,
+                                   int64_t rows, int64_t width, const unsigned long long *offsets,
+                                   uint16_t *x, uint64_t cap, hipStream_t s);
 // counts[t] = cells of slot t (rows [t * slot_rows, (t+1) * slot_rows)) from the extract scan.
 hipError_t launch_extract_slot_counts(const unsigned long long *offsets, int64_t slot_rows,
                                       int64_t slots, unsigned long long *counts, hipStream_t s);

@@ -249,7 +249,9 @@ __global__ void extract_slot_counts(const unsigned long long *__restrict__ offse
 }
 
 // (x, y) of every cell, row-major; a tall board of slots reports y within its slot
-// (y = gy0 + row % slot_rows), slot-major.
+// (y = gy0 + row % slot_rows), slot-major.  X16: x only, as uint16 (width <= 65536; the row of
+// entry i is given by the offsets table, golhip_step_flips_rows) -- a quarter of the bytes.
+template <bool X16>
 __global__ void extract_emit(const uint32_t *__restrict__ a, const uint32_t *__restrict__ b,
                              int64_t pitch, int64_t rows, int32_t nw, uint32_t lastmask,
                              const unsigned long long *__restrict__ offsets, int64_t gy0,
@@ -275,8 +277,12 @@ __global__ void extract_emit(const uint32_t *__restrict__ a, const uint32_t *__r
                 const int bit = __builtin_ctz(v);
                 v &= v - 1;
                 if (pos < cap) {
-                    xy[2 * pos] = col * 32 + bit;
-                    xy[2 * pos + 1] = (int32_t)(gy0 + y % slot_rows);
+                    if constexpr (X16) {
+                        reinterpret_cast<uint16_t *>(xy)[pos] = (uint16_t)(col * 32 + bit);
+                    } else {
+                        xy[2 * pos] = col * 32 + bit;
+                        xy[2 * pos + 1] = (int32_t)(gy0 + y % slot_rows);
+                    }
                 }
                 ++pos;
             }
@@ -438,8 +444,20 @@ hipError_t launch_extract_emit(const uint32_t *a, const uint32_t *b, int64_t pit
     uint32_t lastmask;
     extract_geometry(width, nw, lastmask);
     const unsigned blocks = grid_for(rows * 64, 256, 16384);
-    hipLaunchKernelGGL(extract_emit, dim3(blocks), dim3(256), 0, s, a, b, pitch, rows, nw,
+    hipLaunchKernelGGL(extract_emit<false>, dim3(blocks), dim3(256), 0, s, a, b, pitch, rows, nw,
                        lastmask, offsets, gy0, slot_rows, xy, cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_extract_emit_x16(const uint32_t *a, const uint32_t *b, int64_t pitch,
+                                   int64_t rows, int64_t width, const unsigned long long *offsets,
+                                   uint16_t *x, uint64_t cap, hipStream_t s) {
+    int32_t nw;
+    uint32_t lastmask;
+    extract_geometry(width, nw, lastmask);
+    const unsigned blocks = grid_for(rows * 64, 256, 16384);
+    hipLaunchKernelGGL(extract_emit<true>, dim3(blocks), dim3(256), 0, s, a, b, pitch, rows, nw,
+                       lastmask, offsets, (int64_t)0, rows, reinterpret_cast<int32_t *>(x), cap);
     return hipGetLastError();
 }
 

@@ -42,6 +42,7 @@ EXPORTS = [
     "golhip_set_turn", "golhip_set_k", "golhip_set_band_rows", "golhip_set_tail_bands", "golhip_sync", "golhip_timing",
     "golhip_kernel_time", "golhip_launch_plan", "golhip_launch_kind", "golhip_launch_kind_counts", "golhip_set_fixed_k", "golhip_track_flips",
     "golhip_step_flips", "golhip_flips_ring_capacity", "golhip_flips_fetch",
+    "golhip_step_flips_rows", "golhip_flips_fetch_rows",
     "golhip_checkpoint_save", "golhip_checkpoint_load", "golhip_checkpoint_info",
 ]
 
@@ -179,6 +180,10 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
         "golhip_flips_ring_capacity": ([H, i64p], i32),
         "golhip_flips_fetch": ([H, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
                                 ctypes.c_void_p], i32),
+        "golhip_step_flips_rows": ([H, i64, ctypes.c_void_p, ctypes.c_size_t,
+                                    ctypes.POINTER(ctypes.c_size_t), ctypes.c_void_p, ctypes.c_void_p], i32),
+        "golhip_flips_fetch_rows": ([H, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
+                                     ctypes.c_void_p], i32),
         "golhip_sync": ([H], i32),
         "golhip_timing": ([H, i32], i32),
         "golhip_kernel_time": ([H, ctypes.POINTER(ctypes.c_double), i64p, i64p], i32),
@@ -450,6 +455,40 @@ class Engine:
         bounds = np.concatenate([[0], np.cumsum(per[:turns])]).astype(np.int64)
         out = [xy[bounds[t]:bounds[t + 1]] for t in range(turns)]
         return out, (alive[:turns] if counts else None)
+
+    def step_flips_rows(self, turns: int, counts: bool = False):
+        """golhip_step_flips_rows: (x, row_offsets, alive counts or None), views of page-locked
+        buffers reused by the next call.  x[row_offsets[t*rows + y] : row_offsets[t*rows + y + 1]]
+        are the x of the cells turn t flipped on row y of this handle's strip."""
+        n = ctypes.c_size_t(0)
+        rows = self.info.rows
+        alive = np.zeros(max(turns, 1), dtype=np.uint64) if counts else None
+        offs = getattr(self, "_rows_offs", None)
+        if offs is None or len(offs) < turns * rows + 1:
+            offs = self._rows_offs = pinned_empty((turns * rows + 1,), np.uint64)
+        x = getattr(self, "_rows_x", None)
+        if x is None:
+            x = self._rows_x = pinned_empty((1 << 17,), np.uint16)
+        rc = self._L.golhip_step_flips_rows(self._h, turns, x.ctypes.data, len(x), ctypes.byref(n),
+                                            offs.ctypes.data, alive.ctypes.data if counts else None)
+        if rc == ERR_CAP:
+            x = self._rows_x = pinned_empty((max(n.value, 2 * len(x)),), np.uint16)
+            self._check(self._L.golhip_flips_fetch_rows(self._h, x.ctypes.data, len(x), ctypes.byref(n),
+                                                        offs.ctypes.data))
+        else:
+            self._check(rc)
+        return x[:n.value], offs[:turns * rows + 1], (alive[:turns] if counts else None)
+
+    @staticmethod
+    def rows_to_cells(x, offs, rows: int, turns: int, y0: int = 0):
+        """Expand golhip_step_flips_rows output to per-turn (n_t, 2) int32 (x, y) arrays (tests)."""
+        out = []
+        for t in range(turns):
+            o = offs[t * rows:(t + 1) * rows + 1].astype(np.int64)
+            ys = np.repeat(np.arange(rows, dtype=np.int32) + y0, np.diff(o))
+            xs = x[o[0]:o[-1]].astype(np.int32)
+            out.append(np.stack([xs, ys], axis=1) if len(xs) else np.zeros((0, 2), np.int32))
+        return out
 
     @property
     def turn(self) -> int:

@@ -193,6 +193,18 @@ int golhip_step_flips(golhip_t h, int64_t turns, int32_t *xy, size_t cap, size_t
                       uint64_t *flips_per_turn, uint64_t *alive_per_turn);
 int golhip_flips_ring_capacity(golhip_t h, int64_t *out);
 int golhip_flips_fetch(golhip_t h, int32_t *xy, size_t cap, size_t *n, uint64_t *flips_per_turn);
+/* The same per-turn flips (gol/distributor.go:53-59) in a compact form for consumers that take
+ * rows: x[i] (uint16, width <= 65536) in the same turn-major, row-major order, and
+ * row_offsets[t * rows + y] = the index in x of the first flip of turn t on row y of this
+ * handle's strip (rows = golhip_info.rows; row y is board row golhip_info.y0 + y),
+ * row_offsets[turns * rows] = *n (turns * rows + 1 entries, always written).  2 bytes per flip
+ * instead of an 8-byte (x, y) pair: the list's transfer is what bounds golhip_step_flips on boards
+ * with many flips.  One strip per handle (GOLHIP_ERR_STATE otherwise).  A too-small cap returns
+ * GOLHIP_ERR_CAP with *n and row_offsets set; golhip_flips_fetch_rows returns the cells then.
+ * COLLECTIVE like golhip_step. */
+int golhip_step_flips_rows(golhip_t h, int64_t turns, uint16_t *x, size_t cap, size_t *n,
+                           uint64_t *row_offsets, uint64_t *alive_per_turn);
+int golhip_flips_fetch_rows(golhip_t h, uint16_t *x, size_t cap, size_t *n, uint64_t *row_offsets);
 /* Completed turns since the last load (the broker's `turn`, broker/broker.go:140). */
 int golhip_turn(golhip_t h, int64_t *out);
 int golhip_set_turn(golhip_t h, int64_t turn);

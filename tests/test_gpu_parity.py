@@ -178,6 +178,60 @@ def test_step_flips_sdl_512_every_count(golhip, oracle):
         assert np.array_equal(shadow * 255, e.store())
 
 
+@pytest.mark.parametrize("shape", [(512, 512), (16, 16), (77, 640), (300, 4160)])
+@pytest.mark.parametrize("k", [1, 16])
+def test_step_flips_rows_every_turn(golhip, oracle, shape, k):
+    """golhip_step_flips_rows: the same per-turn flips as golhip_step_flips in the compact form
+    (uint16 x + per-turn-row offsets), expanded and compared with the oracle's per-turn diffs, and
+    interleaved with golhip_step_flips on the same engine (the ring is shared)."""
+    h, w = shape
+    rng = np.random.default_rng(h * 5 + w + k)
+    board = ((rng.random(shape) < 0.4) * 255).astype(np.uint8)
+    with golhip.Engine(w, h, k=k) as e:
+        e.load(board)
+        prev = oracle.to_cells(board)
+        for turns, rows_api in ((17, True), (5, False), (40, True)):
+            if rows_api:
+                x, offs, alive = e.step_flips_rows(turns, counts=True)
+                assert offs[0] == 0 and int(offs[-1]) == len(x)
+                per_turn = e.rows_to_cells(x, offs, h, turns)
+            else:
+                per_turn, alive = e.step_flips(turns, counts=True)
+            for t in range(turns):
+                cur, _ = oracle.packed_run(prev, 1)
+                assert [tuple(c) for c in per_turn[t].tolist()] == oracle.flips(prev, cur), (turns, t)
+                assert int(alive[t]) == int((cur == 255).sum())
+                prev = cur
+        assert np.array_equal(e.store(), prev)
+
+
+def test_step_flips_rows_errors(golhip, oracle):
+    import ctypes
+
+    _, _, board = oracle.read_pgm(REF / "images/64x64.pgm")
+    n = ctypes.c_size_t(0)
+    offs = np.zeros(3 * 64 + 1, np.uint64)
+    with golhip.Engine(64, 64) as e:
+        e.load(board)
+        rc = e._L.golhip_step_flips_rows(e._h, 3, None, 0, ctypes.byref(n), offs.ctypes.data, None)
+        assert rc == golhip.ERR_CAP and n.value > 0 and int(offs[-1]) == n.value
+        x = np.empty(n.value, np.uint16)
+        assert e._L.golhip_flips_fetch_rows(e._h, x.ctypes.data, n.value, ctypes.byref(n), offs.ctypes.data) == 0
+        assert e.turn == 3
+        got = e.rows_to_cells(x, offs, 64, 3)
+        cur = oracle.to_cells(board)
+        for t in range(3):
+            nxt, _ = oracle.packed_run(cur, 1)
+            assert [tuple(c) for c in got[t].tolist()] == oracle.flips(cur, nxt)
+            cur = nxt
+        rc = e._L.golhip_step_flips_rows(e._h, 1, None, 0, ctypes.byref(n), None, None)
+        assert rc == golhip.ERR_ARG  # row_offsets is required
+    with golhip.Engine(64, 64, strips=2) as e:
+        e.load(board)
+        rc = e._L.golhip_step_flips_rows(e._h, 1, None, 0, ctypes.byref(n), offs.ctypes.data, None)
+        assert rc == golhip.ERR_STATE  # one strip per handle
+
+
 def test_step_flips_capacity_errors(golhip, oracle):
     import ctypes
 
