@@ -300,6 +300,9 @@ int setup_engine(golhip_t h, int width, int height, int world, int k) {
     h->split = world > 1;
     h->halo = h->split ? k : 0;
     if (const char *e = std::getenv("GOLHIP_BAND_ROWS")) h->band_rows = std::atoi(e);
+    // measurement knob (scripts/pmc_passes.sh): every bulk launch exactly k deep, as
+    // golhip_set_fixed_k(h, 1) -- the planner would otherwise run its fastest depth <= k
+    if (const char *e = std::getenv("GOLHIP_FIXED_K")) h->fixed_k = std::atoi(e) != 0;
     h->count_window = count_window_env();
     if (const char *e = std::getenv("GOLHIP_SPLIT")) h->force_split = std::atoi(e);
     if (const char *e = std::getenv("GOLHIP_TILE")) h->force_tile = std::atoi(e);

@@ -6,7 +6,7 @@
   * `s` snapshots at 5120^2: golhip_store_bytes between steps (gol/distributor.go:93-103), which
     must issue no hipMalloc/hipFree (the per-shard stage is allocated at create).
 
-Usage: python scripts/flips_profile.py [--calls N] [--snapshots N]"""
+Usage: python scripts/flips_profile.py [--calls N] [--snapshots N] [--rows]"""
 import argparse
 import json
 import sys
@@ -22,18 +22,21 @@ import golhip  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--calls", type=int, default=8)
 ap.add_argument("--snapshots", type=int, default=8)
+ap.add_argument("--rows", action="store_true", help="golhip_step_flips_rows (uint16 x + row offsets)")
 a = ap.parse_args()
 res = {}
 for n in (512, 5120):
     with golhip.Engine(n, n, k=16) as e:
         e.init_random(7)
         T = min(128, e.flips_ring_capacity())
-        e.step_flips(T)  # ring + pinned host list allocated, code paths warm
+        step = (lambda: len(e.step_flips_rows(T)[0])) if a.rows else \
+            (lambda: sum(len(x) for x in e.step_flips(T)[0]))
+        step()  # ring + pinned host list allocated, code paths warm
+        e.init_random(7)
         cells = 0
         t0 = time.perf_counter()
         for _ in range(a.calls):
-            per_turn, _ = e.step_flips(T)
-            cells += sum(len(x) for x in per_turn)
+            cells += step()
         dt = time.perf_counter() - t0
         res[f"flips_{n}"] = {"us_per_turn": round(dt / (a.calls * T) * 1e6, 2), "turns_per_call": T,
                              "flips_per_turn": round(cells / (a.calls * T), 1),
