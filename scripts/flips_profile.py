@@ -40,6 +40,7 @@ for n in (512, 5120):
         dt = time.perf_counter() - t0
         res[f"flips_{n}"] = {"us_per_turn": round(dt / (a.calls * T) * 1e6, 2), "turns_per_call": T,
                              "flips_per_turn": round(cells / (a.calls * T), 1),
+                             "list_bytes_per_call": int(cells / a.calls * (2 if a.rows else 8)),
                              "launch_kind": e.launch_kind(16)}
 with golhip.Engine(5120, 5120, k=16) as e:
     e.init_random(2)
@@ -49,5 +50,5 @@ with golhip.Engine(5120, 5120, k=16) as e:
         e.step(16)
         e.store()
     res["snapshots_5120"] = {"count": a.snapshots,
-                             "ms_per_step16_plus_store": round((time.perf_counter() - t0) / a.snapshots * 1e3, 3)}
+                             "ms_per_step16_plus_store": round((time.perf_counter() - t0) / max(a.snapshots, 1) * 1e3, 3)}
 print(json.dumps(res), flush=True)
