@@ -582,7 +582,11 @@ def main():
             fe.init_random(7)
             cap = fe.flips_ring_capacity()
             T = min(cap, 128)
+            # warm each form on the turns it then times (the host lists are sized by the densest
+            # call, the first: a list that outgrew its buffer inside the timed loop would be
+            # re-allocated and fetched again there)
             fe.step_flips(T)  # allocate the ring, warm
+            fe.init_random(7)
             fe.step_flips_rows(T)
             reps = max(1, 2048 // T)
             cells = 0
