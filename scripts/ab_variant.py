@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Same-process A/B of stencil variants on a pre-heated chip: one engine per variant on the same
 seeded board, advanced in lockstep (same turns, so the same density), rounds alternating the
-variant order; per (variant, k) the median and every round's TCUPS.
+variant order; per (variant, k) the median and every round's TCUPS.  A variant may carry a band
+schedule: "pre63@184:364:176" = bands of 184 rows, the last 364 of 176 (golhip_set_tail_bands).
 Usage: ab_variant.py [size] [ks] [variants] [rounds] [band_rows]"""
 import json
 import os
@@ -22,10 +23,14 @@ rounds = int(sys.argv[4]) if len(sys.argv) > 4 else 7
 band = int(sys.argv[5]) if len(sys.argv) > 5 else 0
 engines = {}
 for v in variants:
-    os.environ["GOLHIP_VARIANT"] = v
+    os.environ["GOLHIP_VARIANT"] = v.split("@")[0]
     e = golhip.Engine(size, size, k=max(ks))
     e.set_fixed_k(True)
     e.set_band_rows(band)
+    if "@" in v:
+        b, n2, b2 = (int(x) for x in v.split("@")[1].split(":"))
+        e.set_band_rows(b)
+        e.set_tail_bands(n2, b2)
     e.init_random(3)
     engines[v] = e
 steps = int(os.environ.get("AB_STEPS", "192"))
