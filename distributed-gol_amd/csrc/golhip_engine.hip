@@ -277,7 +277,7 @@ int64_t plan_rows(golhip_t h) { return strip_plan_rows(h->height, h->world_size)
 // production drift family; gol_step1 at K = 1).  The A/B-experiment variants cannot.
 bool variant_writes_flips(int v) {
     return v == golhip::kVariantProd || v == golhip::kVariantDriftLds || v == golhip::kVariantDrift62 ||
-           v == golhip::kVariantPre63;
+           v == golhip::kVariantPre63 || v == golhip::kVariantProdMask;
 }
 
 int validate_geometry(int width, int height, int world, int k) {
@@ -321,6 +321,7 @@ int setup_engine(golhip_t h, int width, int height, int world, int k) {
                      : std::strcmp(e, "driftnf") == 0 ? golhip::kVariantDriftNoFill
                      : std::strcmp(e, "driftlds") == 0 ? golhip::kVariantDriftLds
                      : std::strcmp(e, "pre63") == 0 ? golhip::kVariantPre63
+                     : std::strcmp(e, "prodmask") == 0 ? golhip::kVariantProdMask
                                                        : golhip::kVariantProd;  // prod
     return GOLHIP_OK;
 }

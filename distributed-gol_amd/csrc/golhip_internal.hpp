@@ -65,12 +65,15 @@ constexpr int kVariantProd = 12;
 // drift with the input rows pre-shifted K bits west (gol_stencil PRE): 63-word chunks, one whole-word
 // store per step, no store realignment (K <= 16; drift62 above)
 constexpr int kVariantPre63 = 13;
-constexpr int kNumVariants = 14;
+// production with the lanes of the last column chunk that nothing depends on exec-masked off
+constexpr int kVariantProdMask = 14;
+constexpr int kNumVariants = 15;
 constexpr bool prod_pre(int K) { return K == 16; }
 // Variants of the production family: gol_step1 at K = 1, the level-split kernel for small boards.
 inline bool variant_is_production_family(int v) {
     return v == kVariantChainLdsPf || v == kVariantDriftLds || v == kVariantDriftZip ||
-           v == kVariantDrift62 || v == kVariantDriftNoFill || v == kVariantProd || v == kVariantPre63;
+           v == kVariantDrift62 || v == kVariantDriftNoFill || v == kVariantProd || v == kVariantPre63 ||
+           v == kVariantProdMask;
 }
 inline int variant_words(int v) {
     return (v == kVariantSkewD2 || v == kVariantChainD2 || v == kVariantSkewLdsD2 ||
@@ -86,7 +89,7 @@ inline int chunk_words(int K, int variant) {
         return 256;  // gol_step1: 4 words x 64 lanes
     const int d = variant_words(variant);
     if (variant == kVariantDriftZip || variant == kVariantDrift62) return 62;
-    if (variant == kVariantProd) return prod_pre(K) ? 63 : 62;
+    if (variant == kVariantProd || variant == kVariantProdMask) return prod_pre(K) ? 63 : 62;
     if (variant == kVariantPre63) return K <= 16 ? 63 : 62;
     return (d == 1 && K <= 16) ? 63 : 62 * d;
 }

@@ -381,8 +381,11 @@ __device__ __forceinline__ void flush_counts(const uint32_t (&acc)[NL], int j0, 
 //             per lane -- the half-word halo's width without its two 16-bit stores.  The shift of
 //             the row and of its west word (2 v_alignbit, the neighbours read from the ring)
 //             replaces the store's realignment (1 DPP + 1 v_alignbit): the same VALU per step.
+// MASK = true: lanes no output or count depends on (past the row end in the last column chunk:
+//             at 65536 wide its 62-word chunk holds 2 words) run the launch exec-masked off, so
+//             they issue nothing into the datapath; the wave's instruction stream is unchanged.
 template <int K, bool COUNT, bool SKEW, int D, int PF, bool HH, bool DR = false, int ZIP = 1,
-          bool FILLU = true, bool LD = false, int WPE = 0, bool PRE = false>
+          bool FILLU = true, bool LD = false, int WPE = 0, bool PRE = false, bool MASK = false>
 // (PRE with counts at K = 16 (production): left alone, the allocator spends 224 VGPRs, i.e. 2 waves
 // per SIMD; held to the half-word-halo kernel's 3 it needs 142 and no scratch.  At K = 12, 4 waves
 // would spill: no hint there.)
@@ -587,6 +590,11 @@ void gol_stencil(const uint32_t *__restrict__ in,
         });
     };
 
+    // MASK: the lanes any stored or counted word depends on -- the west halo lane, the owned and
+    // counted lanes, and (62-word drift) the lane with colraw == wd, whose word is the east
+    // neighbour of the last owned one and holds the wrapped count window
+    const bool live = !MASK || lane == 0 || (PRE ? colraw < p.wd : colraw <= p.wd);
+    if (live) {
     if constexpr (PF == 0) {
         // Register prefetch ring: loads run P steps ahead of their use (deeper for small K,
         // whose steps are short and would otherwise expose HBM latency).
@@ -751,6 +759,7 @@ void gol_stencil(const uint32_t *__restrict__ in,
         // workgroup released its LDS would write into the next workgroup's ring.
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    }  // live
 
     if (COUNT) {
         if (DR && !count_lane) {
@@ -1078,7 +1087,7 @@ inline const void *step1_fn() {
 }
 
 template <int K, bool SKEW, int D, int PF = 0, bool DR = false, int ZIP = 1, bool HH = kHalfHalo<K, D>,
-          bool FILLU = true, bool ALLOW_LD = false, bool PRE = false>
+          bool FILLU = true, bool ALLOW_LD = false, bool PRE = false, bool MASK = false>
 hipError_t launch_stencil_k(const uint32_t *in, uint32_t *out, const StencilParams &p,
                             unsigned long long *slots, hipStream_t s) {
     const int64_t waves = p.nbands * (int64_t)p.nchunks;
@@ -1088,10 +1097,10 @@ hipError_t launch_stencil_k(const uint32_t *in, uint32_t *out, const StencilPara
     if (p.diff) {  // last-generation flips beside the output (production variants only)
         if constexpr (ALLOW_LD) {
             if (slots)
-                hipLaunchKernelGGL((gol_stencil<K, true, SKEW, D, PF, HH, DR, ZIP, FILLU, true, 0, PRE>),
+                hipLaunchKernelGGL((gol_stencil<K, true, SKEW, D, PF, HH, DR, ZIP, FILLU, true, 0, PRE, MASK>),
                                    dim3(blocks), dim3(256), lds_pad_bytes(), s, in, out, p, slots);
             else
-                hipLaunchKernelGGL((gol_stencil<K, false, SKEW, D, PF, HH, DR, ZIP, FILLU, true, 0, PRE>),
+                hipLaunchKernelGGL((gol_stencil<K, false, SKEW, D, PF, HH, DR, ZIP, FILLU, true, 0, PRE, MASK>),
                                    dim3(blocks), dim3(256), lds_pad_bytes(), s, in, out, p, slots);
             return hipGetLastError();
         } else {
@@ -1099,10 +1108,10 @@ hipError_t launch_stencil_k(const uint32_t *in, uint32_t *out, const StencilPara
         }
     }
     if (slots)
-        hipLaunchKernelGGL((gol_stencil<K, true, SKEW, D, PF, HH, DR, ZIP, FILLU, false, 0, PRE>), dim3(blocks), dim3(256),
+        hipLaunchKernelGGL((gol_stencil<K, true, SKEW, D, PF, HH, DR, ZIP, FILLU, false, 0, PRE, MASK>), dim3(blocks), dim3(256),
                            lds_pad_bytes(), s, in, out, p, slots);
     else
-        hipLaunchKernelGGL((gol_stencil<K, false, SKEW, D, PF, HH, DR, ZIP, FILLU, false, 0, PRE>), dim3(blocks), dim3(256),
+        hipLaunchKernelGGL((gol_stencil<K, false, SKEW, D, PF, HH, DR, ZIP, FILLU, false, 0, PRE, MASK>), dim3(blocks), dim3(256),
                            lds_pad_bytes(), s, in, out, p, slots);
     return hipGetLastError();
 }
@@ -1134,6 +1143,10 @@ hipError_t launch_variant(int variant, const uint32_t *in, uint32_t *out, const 
         case kVariantDriftNoFill:
             if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
             else return launch_stencil_k<K, false, 1, 1, (K <= 16), 1, kHalfHalo<K, 1>, false>(in, out, p, slots, s);
+        case kVariantProdMask:  // production with the idle lanes of the last chunk masked off
+            if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
+            else if constexpr (prod_pre(K)) return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true, true, true>(in, out, p, slots, s);
+            else return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true, false, true>(in, out, p, slots, s);
         case kVariantPre63:  // pre-shifted rows, 63-word chunks (K <= 16; drift62 above)
             if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
             else if constexpr (K > 16) return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true>(in, out, p, slots, s);
@@ -1170,6 +1183,10 @@ const void *variant_fn(int variant) {
         case kVariantDriftNoFill:
             if constexpr (K == 1) return step1_fn();
             else return (const void *)gol_stencil<K, false, false, 1, 1, kHalfHalo<K, 1>, (K <= 16), 1, false>;
+        case kVariantProdMask:
+            if constexpr (K == 1) return step1_fn();
+            else if constexpr (prod_pre(K)) return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1, true, false, 0, true, true>;
+            else return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1, true, false, 0, false, true>;
         case kVariantPre63:
             if constexpr (K == 1) return step1_fn();
             else if constexpr (K > 16) return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1>;

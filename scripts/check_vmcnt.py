@@ -36,8 +36,8 @@ from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
 LLVM = Path(os.environ.get("ROCM_PATH", "/opt/rocm")) / "lib" / "llvm" / "bin"
-STENCIL_ARGS = ["K", "COUNT", "SKEW", "D", "PF", "HH", "DR", "ZIP", "FILLU", "LD", "WPE", "PRE"]
-DEFAULTS = {"DR": 0, "ZIP": 1, "FILLU": 1, "LD": 0, "WPE": 0, "PRE": 0}
+STENCIL_ARGS = ["K", "COUNT", "SKEW", "D", "PF", "HH", "DR", "ZIP", "FILLU", "LD", "WPE", "PRE", "MASK"]
+DEFAULTS = {"DR": 0, "ZIP": 1, "FILLU": 1, "LD": 0, "WPE": 0, "PRE": 0, "MASK": 0}
 VMEM = re.compile(r"^(buffer_|global_|scratch_|flat_)")
 
 

@@ -90,7 +90,7 @@ def test_flips_match_oracle(golhip, oracle):
             assert [tuple(c) for c in e.flips().tolist()] == oracle.flips(gen_prev, after), n
 
 
-@pytest.mark.parametrize("variant", ["prod", "driftlds", "drift62", "pre63"])
+@pytest.mark.parametrize("variant", ["prod", "driftlds", "drift62", "pre63", "prodmask"])
 @pytest.mark.parametrize("k", [1, 2, 6, 12, 16, 32])
 @pytest.mark.parametrize("strips", [1, 3])
 def test_tracked_flips_every_depth(golhip, oracle, monkeypatch, variant, k, strips):
@@ -395,7 +395,7 @@ def test_every_kernel_variant(golhip, oracle, monkeypatch, variant, k):
             assert np.array_equal(counts.astype(np.int64), exp_counts), (variant, k, h, w, band)
 
 
-@pytest.mark.parametrize("variant", ["driftlds", "driftzip", "drift62", "pre63"])
+@pytest.mark.parametrize("variant", ["driftlds", "driftzip", "drift62", "pre63", "prodmask"])
 @pytest.mark.parametrize("k", [2, 4, 6, 8, 10, 12, 14, 16, 32])
 def test_drift_variant_every_k(golhip, oracle, monkeypatch, variant, k):
     """The drifting-sum stencils (rows move one bit east per level, one DPP per level update) --
