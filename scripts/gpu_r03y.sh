@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 3 (y): validation of the committed tree: full GPU suite, smoke, the default bench and the
-# driver's 20/5 command
+# driver's 20/5 command; row strips on one GPU as a scheduling device (20-turn A/B)
 set -u
 O=gpurun_out/r03y
 mkdir -p $O
@@ -15,3 +15,5 @@ $G 500 $O/bench.log python3 bench.py || exit $?
 grep "^{" $O/bench.log | cut -c1-200
 $G 400 $O/bench20.log python3 bench.py --gpus 1 --steps 20 --warmup 5 || exit $?
 grep "^{" $O/bench20.log | cut -c1-200
+$G 300 $O/ab_strips.log python3 scripts/ab_strips.py 65536 1,2,4 7 20 || exit $?
+tail -3 $O/ab_strips.log
