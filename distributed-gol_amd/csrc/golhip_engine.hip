@@ -398,9 +398,10 @@ int plan_first_k(int64_t n, int kmax, double cells) {
 
 // Rows per wave band of a stencil launch over rows_total rows.  reserve_waves: resident wave
 // slots to leave free for a concurrent launch (the boundary bands of a split board).
-int64_t auto_band(golhip_t h, int64_t rows_total, int K, int64_t reserve_waves = 0) {
+int64_t auto_band(golhip_t h, int64_t rows_total, int K, int64_t reserve_waves = 0,
+                  bool counting = false) {
     if (h->band_rows > 0) return h->band_rows;
-    const int64_t per = golhip::chunk_words(K, h->variant);
+    const int64_t per = golhip::chunk_words(K, h->variant, counting);
     const int64_t nchunks = (h->wd + per - 1) / per;
     // Fill the chip in whole rounds of resident waves (CUs x resident waves per CU), so every
     // SIMD gets the same number of equal bands.
@@ -549,7 +550,7 @@ RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K, bool counting) 
                      ? prop.multiProcessorCount
                      : 256;
     }
-    const int64_t per = golhip::chunk_words(K, h->variant);
+    const int64_t per = golhip::chunk_words(K, h->variant, counting);
     const int64_t nchunks = (h->wd + per - 1) / per;
     const int64_t minband = std::max(K, 8);
     const int64_t waves1 = (rows_total + minband - 1) / minband * nchunks;
@@ -629,8 +630,10 @@ hipError_t launch_auto(golhip_t h, int K, const uint32_t *in, uint32_t *out,
     return golhip::launch_stencil(K, h->variant, in, out, p, slots, s);
 }
 
+// counting: the launch writes per-generation counts (its kernel, hence its column geometry,
+// can differ: chunk_words / prod_pre)
 StencilParams make_params(golhip_t h, const Shard &s, int K, int64_t r0b, int64_t r0e,
-                          int64_t r1b, int64_t r1e, int64_t reserve_waves = 0) {
+                          int64_t r1b, int64_t r1e, int64_t reserve_waves = 0, bool counting = false) {
     StencilParams p{};
     p.pitch = h->pitch;
     p.r0b = r0b;
@@ -638,7 +641,7 @@ StencilParams make_params(golhip_t h, const Shard &s, int K, int64_t r0b, int64_
     p.r1b = r1b;
     p.r1e = r1e;
     const int64_t total = (r0e - r0b) + (r1e - r1b);
-    p.band = std::min(auto_band(h, std::max<int64_t>(total, 1), K, reserve_waves), max_band_rows(h));
+    p.band = std::min(auto_band(h, std::max<int64_t>(total, 1), K, reserve_waves, counting), max_band_rows(h));
     p.nbands0 = (r0e - r0b + p.band - 1) / p.band;
     // graded bands (golhip_set_tail_bands): range 0 ends in tail_bands bands of tail_rows rows
     const int64_t n2 = h->tail_bands, b2 = h->tail_rows, R0 = r0e - r0b;
@@ -652,7 +655,7 @@ StencilParams make_params(golhip_t h, const Shard &s, int K, int64_t r0b, int64_
     p.lo = -(int64_t)h->halo;
     p.hi = s.rows + h->halo;
     p.wd = h->wd;
-    const int per = golhip::chunk_words(K, h->variant);
+    const int per = golhip::chunk_words(K, h->variant, counting);
     p.nchunks = (h->wd + per - 1) / per;
     return p;
 }
@@ -785,7 +788,7 @@ int step_block(golhip_t h, int K, int64_t slot_gen, int64_t diff_slot = kDiffNon
                          : diff_slot >= 0      ? s.ring + diff_slot * s.rows * h->pitch
                                                : nullptr;
         if (!h->split) {
-            StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0);
+            StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0, 0, slots != nullptr);
             p.diff = diff;
             // a K-deep ring launch (ring_depth: a production register slab) writes the flips of
             // each of its K generations into K consecutive ring slots
@@ -796,9 +799,9 @@ int step_block(golhip_t h, int K, int64_t slot_gen, int64_t diff_slot = kDiffNon
             // boundary bands wait for the halos on their own stream and run concurrently with the
             // interior, in wave slots the interior launch leaves free for them; the compute stream
             // then joins them (counts and the next block need both).
-            StencilParams pb = make_params(h, s, K, 0, K, s.rows - K, s.rows);
+            StencilParams pb = make_params(h, s, K, 0, K, s.rows - K, s.rows, 0, slots != nullptr);
             const int64_t edge_waves = pb.nbands * (int64_t)pb.nchunks;
-            StencilParams pi = make_params(h, s, K, K, s.rows - K, 0, 0, edge_waves);
+            StencilParams pi = make_params(h, s, K, K, s.rows - K, 0, 0, edge_waves, slots != nullptr);
             pb.diff = pi.diff = diff;
             HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, pi, slots, s.compute));
             HIPCHK(h, hipStreamWaitEvent(s.edge, s.ev_halo, 0));
@@ -807,7 +810,7 @@ int step_block(golhip_t h, int K, int64_t slot_gen, int64_t diff_slot = kDiffNon
             HIPCHK(h, hipStreamWaitEvent(s.compute, s.ev_edge, 0));
         } else {
             HIPCHK(h, hipStreamWaitEvent(s.compute, s.ev_halo, 0));
-            StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0);
+            StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0, 0, slots != nullptr);
             p.diff = diff;
             HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, p, slots, s.compute));
         }
@@ -1066,7 +1069,7 @@ struct LaunchPlanner {
 
 int graph_for(golhip_t h, int K, int M, bool counting, hipGraphExec_t *out) {
     Shard &s = h->shards[0];
-    const int64_t band = auto_band(h, s.rows, K);
+    const int64_t band = auto_band(h, s.rows, K, 0, counting);
     for (auto &g : h->graphs)
         if (g.K == K && g.M == M && g.cur == h->cur && g.counting == counting && g.band == band) {
             *out = g.exec;
@@ -1080,7 +1083,7 @@ int graph_for(golhip_t h, int K, int M, bool counting, hipGraphExec_t *out) {
     hipError_t err = hipSuccess;
     for (int i = 0; i < M && err == hipSuccess; ++i) {
         const int c = h->cur ^ (i & 1);
-        StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0);
+        StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0, 0, counting);
         err = launch_auto(h, K, h->row0(s, c), h->row0(s, c ^ 1), p,
                           counting ? s.slots + (int64_t)i * K * golhip::kCountSlots : nullptr,
                           s.compute);

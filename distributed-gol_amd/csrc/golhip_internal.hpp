@@ -68,7 +68,11 @@ constexpr int kVariantPre63 = 13;
 // production with the lanes of the last column chunk that nothing depends on exec-masked off
 constexpr int kVariantProdMask = 14;
 constexpr int kNumVariants = 15;
-constexpr bool prod_pre(int K) { return K == 16; }
+// The pre-shifted geometry in production: every non-counting launch of depth 2..16 (the driver's
+// dense 20-turn region, pre-heated: +1.2 % over the 62-word chunks, profiles/r03/r03aa_ab_split.log;
+// K = 16 +2.9 %), and counting launches at K = 16 only (with counts at K < 16 its allocator holds
+// 168 VGPRs, 3 waves per SIMD, against the 62-word kernel's 110 and 4).
+constexpr bool prod_pre(int K, bool counting = false) { return K == 16 || (!counting && K >= 2 && K < 16); }
 // Variants of the production family: gol_step1 at K = 1, the level-split kernel for small boards.
 inline bool variant_is_production_family(int v) {
     return v == kVariantChainLdsPf || v == kVariantDriftLds || v == kVariantDriftZip ||
@@ -84,12 +88,12 @@ inline int variant_words(int v) {
 // Words of a row owned by one wave of the stencil (its column chunk): 62 lanes x D words, or 63
 // words with the half-word halo (D = 1, K <= 16: lanes 0 and 63 own half a word each).
 constexpr int kStep1WavesPerCu = 8;  // gol_step1 grid: resident waves per CU it is sized for
-inline int chunk_words(int K, int variant) {
+inline int chunk_words(int K, int variant, bool counting = false) {
     if (K == 1 && variant_is_production_family(variant))
         return 256;  // gol_step1: 4 words x 64 lanes
     const int d = variant_words(variant);
     if (variant == kVariantDriftZip || variant == kVariantDrift62) return 62;
-    if (variant == kVariantProd || variant == kVariantProdMask) return prod_pre(K) ? 63 : 62;
+    if (variant == kVariantProd || variant == kVariantProdMask) return prod_pre(K, counting) ? 63 : 62;
     if (variant == kVariantPre63) return K <= 16 ? 63 : 62;
     return (d == 1 && K <= 16) ? 63 : 62 * d;
 }

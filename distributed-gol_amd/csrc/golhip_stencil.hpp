@@ -1136,17 +1136,23 @@ hipError_t launch_variant(int variant, const uint32_t *in, uint32_t *out, const 
         case kVariantDrift62:
             if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
             else return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true>(in, out, p, slots, s);
-        case kVariantProd:  // per depth: the fastest measured (golhip_internal.hpp)
+        case kVariantProd:  // per depth and counting: the fastest measured (golhip_internal.hpp)
             if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
-            else if constexpr (prod_pre(K)) return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true, true>(in, out, p, slots, s);
-            else return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true>(in, out, p, slots, s);
+            else if constexpr (K <= 16) {
+                if (prod_pre(K, slots != nullptr))
+                    return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true, true>(in, out, p, slots, s);
+                return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true>(in, out, p, slots, s);
+            } else return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true>(in, out, p, slots, s);
         case kVariantDriftNoFill:
             if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
             else return launch_stencil_k<K, false, 1, 1, (K <= 16), 1, kHalfHalo<K, 1>, false>(in, out, p, slots, s);
         case kVariantProdMask:  // production with the idle lanes of the last chunk masked off
             if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
-            else if constexpr (prod_pre(K)) return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true, true, true>(in, out, p, slots, s);
-            else return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true, false, true>(in, out, p, slots, s);
+            else if constexpr (K <= 16) {
+                if (prod_pre(K, slots != nullptr))
+                    return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true, true, true>(in, out, p, slots, s);
+                return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true, false, true>(in, out, p, slots, s);
+            } else return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true, false, true>(in, out, p, slots, s);
         case kVariantPre63:  // pre-shifted rows, 63-word chunks (K <= 16; drift62 above)
             if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
             else if constexpr (K > 16) return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true>(in, out, p, slots, s);
