@@ -417,6 +417,28 @@ def test_drift_variant_every_k(golhip, oracle, monkeypatch, variant, k):
             assert count == int((exp == 255).sum())
 
 
+@pytest.mark.parametrize("k", [2, 8, 12, 14, 16])
+def test_counting_and_plain_launches_interleaved(golhip, oracle, k):
+    """Production picks the column geometry per launch (pre-shifted 63-word chunks without counts,
+    62-word chunks with counts below K = 16): steps with and without per-turn counts interleaved
+    on one engine, streaming kernel (explicit band height), equal to the oracle after each."""
+    for (h, w, band) in [(300, 4160, 40), (97, 2016, 24), (64, 65536, 16)]:
+        rng = np.random.default_rng(h + w + k)
+        board = ((rng.random((h, w)) < 0.4) * 255).astype(np.uint8)
+        with golhip.Engine(w, h, k=k) as e:
+            e.set_fixed_k(True)
+            e.set_band_rows(band)
+            e.load(board)
+            cur = oracle.to_cells(board)
+            for n, counts in ((2 * k + 1, True), (k + 3, False), (k, True), (3 * k, False)):
+                c = e.step(n, counts=counts)
+                exp, exp_counts = oracle.packed_run(cur, n)
+                assert np.array_equal(e.store(), exp), (k, h, w, n, counts)
+                if counts:
+                    assert np.array_equal(c.astype(np.int64), exp_counts), (k, h, w, n)
+                cur = exp
+
+
 @pytest.mark.parametrize("k", [1, 2, 8, 12, 16])
 def test_graded_tail_bands(golhip, oracle, k):
     """Graded bands (golhip_set_tail_bands): range 0 ends in short bands after the full-height
