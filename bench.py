@@ -546,9 +546,10 @@ def main():
             # scripts/diag_k1.py), so k = 1 gets a longer untimed warmup
             eng.step(256 if kk == 1 else 2 * kk)
             n = max(4 * kk, 256)
-            eng.timing(kk == 1)
-            t = timed_steps(eng, n, 1)
-            if kk == 1:
+            t = timed_steps(eng, n, 1)  # uninstrumented (events between launches cost time)
+            if kk == 1:  # the k = 1 launch duration for hbm_roofline_k1: a separate evented run
+                eng.timing(True)
+                timed_steps(eng, n, 1)
                 ms1, l1, _ = eng.kernel_time()
                 k1_launch_us = ms1 * 1e3 / max(l1, 1)
                 eng.timing(False)
