@@ -344,9 +344,22 @@ int pick_k(int n) {
 // ranking: at 262144^2 (2096-row bands) K = 16 runs 129 vs 122 at K = 12, while every smaller
 // streaming board measured runs K = 12 faster (16384^2 +17 %, 32768^2 +9.5 %, 65536^2 +2.3 %,
 // 131072^2 +3 %: r02ae/r02af).  Only the ranking and the ratios matter to the planner.
+// Round 3: with the pre-shifted geometry on every non-counting launch, strips of 2^31 .. 2^35
+// cells (65536^2 and up) rank K = 14 first: 125.5-125.8 vs 123.8-124.3 (K = 12) and 124.0-124.8
+// (K = 16) TCUPS in a lockstep A/B and two default-bench k sweeps (profiles/r03/r03ae_*,
+// r03ab_bench.json, r03ah_bench.json); smaller streaming boards (graph replays) keep K = 12.
 constexpr double kLargeStripCells = 34359738368.0;  // 2^35
+constexpr double kMidStripCells = 2147483648.0;     // 2^31
 double launch_rate_tcups(int K, double cells = 0.0) {
     const bool large = cells >= kLargeStripCells;
+    if (!large && cells >= kMidStripCells) {
+        switch (K) {
+            case 12: return 124.1;
+            case 14: return 125.6;
+            case 16: return 124.4;
+            default: break;
+        }
+    }
     switch (K) {
         case 1: return 22.8;
         case 2: return 35.4;

@@ -111,17 +111,22 @@ def test_launch_plan_long_runs_replay_large_graphs(golhip):
 
 
 def test_launch_plan_bulk_depth_by_board_size(golhip):
-    """The bulk depth follows the strip size (profiles/r02/r02ae_depth_by_size.txt, pre-heated
-    chip): K = 12 on streaming boards below 2^35 cells per strip (5 resident waves per SIMD, an
-    11-row band trapezoid), K = 16 on larger strips (262144^2: 129 vs 122 TCUPS); small streaming
-    boards replay graphs of 12-deep launches, register-slab boards of 16-deep ones."""
+    """The bulk depth follows the strip size (profiles/r02/r02ae_depth_by_size.txt and round 3's
+    pre-shifted geometry, pre-heated chip): K = 14 on strips of 2^31 .. 2^35 cells (65536^2: 125.6
+    vs 124.1 at K = 12), K = 12 below (graph-replayed streaming boards), K = 16 on larger strips
+    (262144^2: 139 vs 138 at K = 14); register-slab boards replay graphs of 16-deep launches."""
     from collections import Counter
 
-    assert Counter(golhip.launch_plan(65536, 65536, 16, 1008)) == {12: 84}
-    assert Counter(golhip.launch_plan(131072, 131072, 16, 480)) == {12: 40}
+    assert Counter(golhip.launch_plan(65536, 65536, 16, 1008)) == {14: 72}
+    p131 = golhip.launch_plan(131072, 131072, 16, 480)
+    assert sum(p131) == 480 and Counter(p131)[14] >= 32
     assert Counter(golhip.launch_plan(262144, 262144, 16, 160)) == {16: 10}
-    # per strip: the 262144^2 board over 8 ranks is 2^33 cells per strip -> K = 12
-    assert set(golhip.launch_plan(262144, 262144, 16, 480, strips=8)) == {12}
+    # per strip: the 262144^2 board over 8 ranks is 2^33 cells per strip -> K = 14 in bulk
+    p8 = golhip.launch_plan(262144, 262144, 16, 480, strips=8)
+    assert sum(p8) == 480 and Counter(p8)[14] >= 32
+    # the driver's 20-turn region stays 12 + 8 (a 6-deep launch runs at ~3/4 the rate)
+    assert sorted(golhip.launch_plan(65536, 65536, 16, 20)) == [8, 12]
+    assert sorted(golhip.launch_plan(65536, 131072, 16, 20, strips=2)) == [8, 12]
     graphs16k = [-d for d in golhip.launch_plan(16384, 16384, 16, 2000) if d < 0]
     assert graphs16k and set(graphs16k) == {120}  # 10 launches of K = 12 per replay
     graphs5k = [-d for d in golhip.launch_plan(5120, 5120, 16, 10000) if d < 0]
