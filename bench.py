@@ -22,11 +22,16 @@ Prints ONE JSON line on rank 0 (keys per the driver contract), plus:
   hbm_roofline : the algorithmic-HBM figure of the same timed launches (exceeds 1 for k > 1:
                  temporal blocking reads and writes the board once per k generations);
   parity       : alive cells after warmup + steps generations == the oracle's golden count
-                 (tests/golden/cfg3_65536_seed3_counts.csv) when that turn is pinned;
+                 (tests/golden/cfg3_65536_seed3_counts.csv) when that turn is pinned, and the
+                 whole board's digest (SHA-256 of 4096-row chunk SHA-256s, each rank hashing its
+                 own strip after the timed pass) == the oracle's (tests/golden synthetic_golden.json
+                 digest_65536x*, turns 25 and 1008): bit-exact, not only count-exact;
   cpu_baseline : the reference algorithm (oracle/ port of server/server.go + broker split,
-                 byte per cell, 4 servers x 4 threads, full-world fan-out copy per server per
-                 turn, per-turn alive scan) timed on this host on a bounded sample of the same
-                 65536^2 board, plus configs[0] (512^2 x 100 turns) in full;
+                 byte per cell, 4 servers x T goroutine-threads from a persistent pool, full-world
+                 fan-out copy per server per turn, per-turn alive scan) timed on this host: a T sweep
+                 (T = 1, 2, 4, 8, 16, the cgroup quota / 4 and every host core / 4) on configs[0]
+                 (512^2 x 100, bit-exact) and the first 20 turns of configs[1]; the bench board at the
+                 best T; configs[4]'s first turns; configs[3] (262144^2) extrapolated;
   k_sweep      : GCUPS per temporal-blocking depth k (N == 1 only);
   hbm_roofline_k1: the k = 1 kernel (gol_step1, no temporal reuse) against the HBM peak;
   strong_262144: configs[3] -- the 262144^2 board (seed 4) split over the N ranks, GCUPS and
@@ -44,6 +49,8 @@ value is the loaded-clock rate and cold_start keeps the idle-start figure beside
 from __future__ import annotations
 
 import argparse
+import datetime
+import hashlib
 import json
 import os
 import sys
@@ -89,8 +96,8 @@ def parse():
     ap.add_argument("--cpu-size", type=int, default=65536, help="CPU baseline board (the bench board)")
     ap.add_argument("--cpu-turns", type=int, default=2, help="CPU baseline turns (~15 s of CPU work)")
     ap.add_argument("--cpu-threads-per-server", type=int, default=0,
-                    help="goroutine-threads per reference server in the CPU baseline "
-                         "(0 = ceil(host CPUs / 4): every host core)")
+                    help="goroutine-threads per reference server for the CPU baseline's bench-board "
+                         "sample (0 = the best T of its sweep)")
     ap.add_argument("--no-timing", action="store_true",
                     help="no per-launch HIP events in the timed region (roofline from wall time)")
     ap.add_argument("--pmc-file", default=str(ROOT / "profiles" / "pmc_traffic.json"))
@@ -101,6 +108,16 @@ def parse():
                     help="skip the configs[0]/[1]/[4] leg (512^2 PGM, 5120^2 and 4096^2 with every count)")
     ap.add_argument("--strong-size", type=int, default=262144)
     ap.add_argument("--strong-steps", type=int, default=160)
+    ap.add_argument("--fixed-k", action="store_true",
+                    help="every bulk launch exactly --k deep (PMC passes at one depth; the planner "
+                         "otherwise runs its fastest measured depth <= k)")
+    ap.add_argument("--pg-timeout-s", type=float, default=120.0,
+                    help="torch.distributed process-group timeout at N > 1 (well under a driver's "
+                         "600 s bench limit: a stuck collective fails the run instead of hanging it)")
+    ap.add_argument("--comm-timeout-ms", type=int, default=120000,
+                    help="libgolhip's RCCL deadline (golhip_set_comm_timeout): a halo exchange, "
+                         "all-reduce or communicator set-up that does not complete fails with "
+                         "GOLHIP_ERR_RCCL naming the pending transfer")
     ap.add_argument("--preheat-ms", type=float, default=200.0,
                     help="after a cold-start pass of the same turns (reported as cold_start), "
                          "untimed K-deep launches for this long, then the board is re-initialised "
@@ -172,71 +189,155 @@ def cpu_share() -> dict:
 def cpu_baseline(size: int, turns: int, threads_per_server: int | None = None) -> dict:
     """The reference's algorithm (oracle/gol_oracle.c oracle_ref_*), timed on this host.
 
-    Sample: `turns` turns of the bench board itself (65536^2 random, seed 3) with the reference's
-    cost structure -- byte cells, branchy torus wrap + /255, fresh rows per turn, 4 broker strips
-    x `threads_per_server` goroutine-threads, a private full-world copy per server per turn (the
-    gob fan-out of broker/broker.go:51,64; each server copies its own, concurrently)
-    and the controller's per-turn alive scan (gol/distributor.go:186).  The RPC transport itself
-    (gob encode/TCP) is not timed.  threads_per_server defaults to ceil(host CPUs / 4): T = every
-    host core (each reference server runs req.Threads goroutines,
-    server/server.go:83-97).  Plus configs[0] in full: images/512x512.pgm for 100 turns, checked
-    byte-exact against the reference's check/images/512x512x100.pgm."""
+    The reference's cost structure: byte cells, branchy torus wrap + /255, fresh rows per turn,
+    4 broker strips x T goroutine-threads (server/server.go:83-97, req.Threads per server), a
+    private full-world copy per server per turn (the gob fan-out of broker/broker.go:51,64; each
+    server copies its own, concurrently) and the controller's per-turn alive scan
+    (gol/distributor.go:186).  The workers are a persistent pool handed each turn through
+    barriers -- the goroutine analogue (round 3 created 4T OS threads per turn).  The RPC
+    transport itself (gob encode/TCP) is not timed.
+
+    Legs (sample sizes chosen to keep the whole leg ~30 s):
+      sweep   : T = 1, 2, 4, 8, 16 (the reference's own thread matrix, gol_test.go:29), T = the
+                cgroup CPU quota / 4 and T = every host CPU / 4: configs[0] in full (512^2 x 100,
+                bit-exact vs check/images/512x512x100.pgm) and the first 20 turns of configs[1]
+                (5120^2 seed 2, every count vs the golden CSV);
+      value   : `turns` turns of the bench board itself (65536^2 random p=0.5 seed 3) at the best T
+                of the configs[1] prefix (or threads_per_server when given);
+      cfg5    : the first 100 turns of configs[4] (4096^2 gun + R-pentomino), every count checked;
+      cfg4    : configs[3] (262144^2) is NOT run: its byte board needs 64 GiB per copy (world, next,
+                4 fan-out copies: 384 GiB > the job's host-memory cap); one turn is extrapolated
+                from the bench board's per-cell rate (labelled)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import numpy as np
 
     import oracle
 
     nproc, model = host_cpu()
-    if threads_per_server is None:
-        threads_per_server = max(1, -(-nproc // 4))
-    threads = 4 * threads_per_server
-    # configs[0] in full
+    share = cpu_share()
+    quota = share.get("cgroup_cpu_quota")
+    t_quota = max(1, round(quota / 4)) if quota else None
+    t_cores = max(1, -(-nproc // 4))
     ref = GOLDEN / "reference"
-    _, _, b512 = oracle.read_pgm(ref / "images" / "512x512.pgm")
-    t0 = time.perf_counter()
-    out512, _ = oracle.ref_run(b512, 100, threads=threads_per_server, servers=4, fanout_copy=True)
-    dt512 = time.perf_counter() - t0
-    exact = oracle.pgm_bytes(out512) == (ref / "check" / "images" / "512x512x100.pgm").read_bytes()
-
-    # configs[1] prefix: 5120^2 seed 2, the first 20 of its 10 000 turns, every count checked
-    # against the golden CSV (the oracle's own per-turn counts)
     gold = json.loads((GOLDEN / "synthetic_golden.json").read_text())
+    _, _, b512 = oracle.read_pgm(ref / "images" / "512x512.pgm")
+    want512 = (ref / "check" / "images" / "512x512x100.pgm").read_bytes()
     lines = (GOLDEN / gold["cfg2"]["counts_csv"]).read_text().split()[1:21]
+    want2 = [int(ln.split(",")[1]) for ln in lines]
     b2 = oracle.unpack(oracle.init_random(5120, 5120, seed=2), 5120)
-    t0 = time.perf_counter()
-    _, c2 = oracle.ref_run(b2, 20, threads=threads_per_server, servers=4, fanout_copy=True)
-    dt2 = time.perf_counter() - t0
-    ok2 = [int(x) for x in c2] == [int(ln.split(",")[1]) for ln in lines]
+
+    sweep = {}
+    for T in sorted({1, 2, 4, 8, 16, t_cores} | ({t_quota} if t_quota else set())):
+        t0 = time.perf_counter()
+        out512, _ = oracle.ref_run(b512, 100, threads=T, servers=4, fanout_copy=True)
+        dt512 = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        _, c2 = oracle.ref_run(b2, 20, threads=T, servers=4, fanout_copy=True)
+        dt2 = time.perf_counter() - t0
+        labels = [x for x, v in (("quota", t_quota), ("host_cores", t_cores)) if v == T]
+        sweep[str(T)] = {"os_threads": 4 * T, "label": labels or None,
+                         "cfg1_512x100_s": round(dt512, 4),
+                         "cfg1_gcups": round(512 * 512 * 100 / dt512 / 1e9, 4),
+                         "cfg1_bit_exact": oracle.pgm_bytes(out512) == want512,
+                         "cfg2_first20_s": round(dt2, 4),
+                         "cfg2_gcups": round(5120 * 5120 * 20 / dt2 / 1e9, 4),
+                         "cfg2_counts_match": [int(x) for x in c2] == want2}
     del b2
+    best_t = max(sweep, key=lambda t: sweep[t]["cfg2_gcups"])
+    T = threads_per_server or int(best_t)
 
     board = oracle.unpack(oracle.init_random(size, size, seed=3), size)
     t0 = time.perf_counter()
-    oracle.ref_run(board, turns, threads=threads_per_server, servers=4, fanout_copy=True)
+    oracle.ref_run(board, turns, threads=T, servers=4, fanout_copy=True)
     dt = time.perf_counter() - t0
+    del board
     cups = size * size * turns / dt
-    del board, np
+
+    # configs[4]: the first 100 turns, every count vs the golden npz
+    b5 = np.zeros((4096, 4096), dtype=np.uint8)
+    golhip.place(b5, golhip.parse_rle((GOLDEN / "gosper_gun.rle").read_text()), 64, 64)
+    golhip.place(b5, golhip.parse_rle((GOLDEN / "r_pentomino.rle").read_text()), 2048, 2048)
+    deltas = np.load(GOLDEN / gold["cfg5"]["counts_1e6_npz"])["deltas"][:100]
+    exp5 = (int((b5 == 255).sum()) + np.cumsum(deltas.astype(np.int64))).tolist()
+    t0 = time.perf_counter()
+    _, c5 = oracle.ref_run(b5, 100, threads=T, servers=4, fanout_copy=True)
+    dt5 = time.perf_counter() - t0
+
+    n4 = 262144
     return {
         "value": round(cups / 1e9, 4),
         "unit": "GCUPS",
-        "cores": threads,
+        "cores": 4 * T,
+        "threads_per_server": T,
         "host_cores": nproc,
-        **cpu_share(),
+        **share,
         "cpu_model": model,
         "fanout_copy": True,
+        "workers": "persistent pool (goroutine analogue): 4 servers x T threads created once per run",
         "kind": "port",
         "sample": (f"{size}x{size} random p=0.5 seed 3 (the bench board), {turns} turns of the "
-                   f"reference algorithm: byte cells, branchy torus wrap + /255, fresh rows per "
-                   f"turn, 4 broker strips x {threads_per_server} goroutine-threads = {threads} OS "
-                   f"threads, full-world copy per server per turn, per-turn alive scan; gob/TCP "
-                   f"transport not timed; {dt:.1f} s; threads = every host CPU (os.cpu_count()), "
-                   f"which on a shared GPU box may exceed the job's CPU quota (cgroup_cpu_quota)"),
-        "cfg1_512x100": {"s": round(dt512, 4), "gcups": round(512 * 512 * 100 / dt512 / 1e9, 4),
-                         "bit_exact_vs_reference_fixture": bool(exact)},
-        "cfg2_5120_first20": {"s": round(dt2, 4), "gcups": round(5120 * 5120 * 20 / dt2 / 1e9, 4),
-                              "us_per_turn": round(dt2 / 20 * 1e6, 1),
-                              "counts_match_golden": bool(ok2),
-                              "sample": "first 20 of configs[1]'s 10 000 turns (labelled prefix)"},
+                   f"reference algorithm at T = {T} goroutine-threads per server (the best T of the "
+                   f"sweep on configs[1]'s first 20 turns): byte cells, branchy torus wrap + /255, "
+                   f"fresh rows per turn, 4 broker strips x {T} = {4 * T} worker threads (one pool "
+                   f"per run), full-world copy per server per turn, per-turn alive scan; gob/TCP "
+                   f"transport not timed; {dt:.1f} s"),
+        "t_sweep": sweep,
+        "best_threads_per_server": int(best_t),
+        "cfg5_4096_first100": {"s": round(dt5, 4), "gcups": round(4096 * 4096 * 100 / dt5 / 1e9, 4),
+                               "us_per_turn": round(dt5 / 100 * 1e6, 1),
+                               "counts_match_golden": [int(x) for x in c5] == exp5,
+                               "sample": "first 100 of configs[4]'s 1e6 turns (labelled prefix)"},
+        "cfg4_262144_extrapolated": {
+            "s_per_turn": round(n4 * n4 / cups, 2), "gcups": round(cups / 1e9, 4),
+            "note": ("not run: the byte board needs 64 GiB per copy (world, next and 4 fan-out "
+                     "copies = 384 GiB, over the job's host-memory cap); extrapolated from the "
+                     f"{size}^2 sample's per-cell rate (labelled extrapolation)")},
     }
+
+
+DIGEST_CHUNK_ROWS = 4096  # = oracle.DIGEST_CHUNK_ROWS (tests/test_bench_digest.py checks both)
+
+
+def chunk_digests(words) -> list[bytes]:
+    """SHA-256 of each 4096-row chunk of packed little-endian uint64 rows (a strip's share of the
+    board digest; the oracle's definition, restated here so the bench's GPU path imports no oracle)."""
+    import numpy as np
+
+    w = np.ascontiguousarray(words, dtype="<u8")
+    return [hashlib.sha256(w[y:y + DIGEST_CHUNK_ROWS].tobytes()).digest()
+            for y in range(0, w.shape[0], DIGEST_CHUNK_ROWS)]
+
+
+def board_digest(eng: golhip.Engine, world: int) -> str | None:
+    """SHA-256 of the chunk digests of the whole board (every rank's strip, in row order), or None
+    when a strip does not start on a chunk boundary or the width is not a multiple of 64."""
+    info = eng.info
+    mine = None
+    if info.width % 64 == 0 and info.y0 % DIGEST_CHUNK_ROWS == 0:
+        mine = chunk_digests(eng.store_words())
+    if world > 1:
+        parts = [None] * world
+        dist.all_gather_object(parts, mine)
+    else:
+        parts = [mine]
+    if any(p is None for p in parts):
+        return None
+    return hashlib.sha256(b"".join(c for p in parts for c in p)).hexdigest()
+
+
+def golden_digest(width: int, height: int, seed: int, turn: int) -> str | None:
+    """The oracle's board digest of the width x height random board (p = 0.5, `seed`) after `turn`
+    turns, if tests/golden/synthetic_golden.json pins it (scripts/make_golden.py digests)."""
+    try:
+        gold = json.loads((GOLDEN / "synthetic_golden.json").read_text())
+    except OSError:
+        return None
+    for entry in gold.values():
+        if (entry.get("width"), entry.get("height"), entry.get("seed")) == (width, height, seed):
+            d = entry.get("board_digest", {}).get(str(turn))
+            if d:
+                return d
+    return None
 
 
 def golden_count(width: int, height: int, seed: int, turn: int) -> int | None:
@@ -359,6 +460,9 @@ def configs_leg() -> dict:
     return res
 
 
+ENGINES: list = []  # the engines this process created (their last C ABI call names a failure)
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -379,7 +483,9 @@ def main():
         # RCCL id broadcast) over RCCL; gloo where RCCL cannot run (the host-transport hook's
         # ranks share one GPU; CPU-only test runs)
         backend = "nccl" if torch.cuda.is_available() and not host_comm else "gloo"
-        dist.init_process_group(backend, rank=rank, world_size=world)
+        dist.init_process_group(backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=a.pg_timeout_s))
+    golhip.set_default_comm_timeout(a.comm_timeout_ms)
 
     width = a.size
     height = a.height or a.size * world
@@ -390,8 +496,11 @@ def main():
         nccl_id = obj[0]
     eng = golhip.Engine(width, height, k=a.k, rank=rank, world_size=world, device=local,
                         nccl_id=nccl_id, host_comm=golhip.GlooHostComm() if host_comm else None)
+    ENGINES.append(eng)
     if a.band_rows:
         eng.set_band_rows(a.band_rows)
+    if a.fixed_k:
+        eng.set_fixed_k(True)
     eng.init_random(a.seed)
     local_rows = eng.info.rows
     cold = None
@@ -436,6 +545,9 @@ def main():
     # regression canary: alive cells after exactly warmup + steps generations (deterministic for
     # the seed; compare across kernel versions)
     alive_timed = eng.alive_count()
+    # the whole board after the timed pass, bit for bit: every rank hashes its strip in 4096-row
+    # chunks (outside the timed region), rank 0 hashes the gathered chunk digests
+    digest = board_digest(eng, world)
     instrumented = None
     if a.no_timing:
         launches = -(-a.steps // a.k)
@@ -534,6 +646,13 @@ def main():
             if cold is not None:
                 parity["cold_start_ok"] = cold["alive_after"] == exp
                 parity["ok"] = parity["ok"] and parity["cold_start_ok"]
+    exp_digest = golden_digest(width, height, a.seed, a.warmup + a.steps)
+    if exp_digest is not None:
+        parity = parity or {"turn": a.warmup + a.steps, "ok": True}
+        parity["digest"] = digest
+        parity["golden_digest"] = exp_digest
+        parity["digest_ok"] = digest == exp_digest
+        parity["ok"] = parity["ok"] and parity["digest_ok"]
 
     sweep = None
     k1_launch_us = None
@@ -573,6 +692,7 @@ def main():
             sid = obj[0]
         se = golhip.Engine(n, n, k=a.k, rank=rank, world_size=world, device=local, nccl_id=sid,
                            host_comm=golhip.GlooHostComm() if host_comm else None)
+        ENGINES.append(se)
         se.init_random(4)
         se.step(a.k)
         se.sync()
@@ -705,8 +825,17 @@ def main():
     bad = ((parity and not parity["ok"]) or (strong and strong.get("parity") and not strong["parity"]["ok"])
            or (small and not small["ok"]))
     if bad:
-        raise SystemExit("bench parity FAILED: alive count differs from the oracle's golden count")
+        raise SystemExit("bench parity FAILED: the board (alive count or digest) differs from the oracle's")
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except SystemExit:
+        raise
+    except BaseException as e:  # a failed engine call or collective: say where, exit non-zero
+        rank = os.environ.get("RANK", "0")
+        calls = ", ".join(f"{getattr(x, 'last_call', '?')}" for x in ENGINES) or "none"
+        print(f"bench: rank {rank} failed: {e!r}; last engine call(s): {calls}", file=sys.stderr,
+              flush=True)
+        raise SystemExit(3)

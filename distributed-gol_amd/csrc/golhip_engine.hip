@@ -14,6 +14,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -21,6 +23,7 @@
 #include <cstring>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/golhip.h"
@@ -30,14 +33,16 @@ using golhip::StencilParams;
 
 namespace {
 
-constexpr int kVersion = 100;
-// Generations of per-turn counts finalized per launch (GOLHIP_COUNT_WINDOW, read at create,
-// overrides it; at least the graph length kGraphGens: tests shrink it to exercise flushes).
-int count_window_env() {
-    const char *e = std::getenv("GOLHIP_COUNT_WINDOW");
-    const int v = e ? std::atoi(e) : 4096;
-    return v < 128 ? 128 : v;
-}
+constexpr int kVersion = 101;
+// Generations of per-turn counts finalized per launch (golhip_set_count_window changes it; at
+// least the graph length kGraphGens: tests shrink it to exercise flushes).
+constexpr int kCountWindowDefault = 4096;
+constexpr int kCountWindowMin = 128;
+// Default deadline of a host wait on RCCL-dependent work and of the communicator's set-up
+// (golhip_set_comm_timeout(NULL, ms) changes it for later creates): well under the 600 s a driver
+// gives a whole bench run, far above any legitimate wait (an 8-rank init takes seconds, a K-row
+// exchange microseconds; stencil work queued by the host is added to each wait by its model).
+std::atomic<int64_t> g_comm_timeout_ms{120000};
 
 struct Shard {
     int device = 0;
@@ -83,6 +88,7 @@ struct GraphEntry {
     int K = 0, M = 0, cur = 0;
     bool counting = false;
     int64_t band = 0;
+    int tail_bands = 0, tail_rows = 0;  // golhip_set_tail_bands at capture
     hipGraphExec_t exec = nullptr;
 };
 
@@ -110,9 +116,24 @@ struct golhip_engine {
     golhip_host_comm host_comm{};
     void *hc_buf[4] = {nullptr, nullptr, nullptr, nullptr};
     bool split = false;  // board held as halo'd row strips (world > 1, or GOLHIP_RING_SELF)
-    int force_split = 0;  // GOLHIP_SPLIT (0 = automatic)
-    int force_tile = -1;  // GOLHIP_TILE: -1 automatic, 0 never, T > 0 always (tile height T)
-    int force_slab = -1;  // GOLHIP_SLAB: -1 automatic, 0 never, W*100 + S always (slab shape)
+    // tuning build only (GOLHIP_SPLIT / GOLHIP_TILE / GOLHIP_SLAB); the production build keeps the
+    // automatic choice
+    int force_split = 0;  // 0 = automatic
+    int force_tile = -1;  // -1 automatic, 0 never, T > 0 always (tile height T)
+    int force_slab = -1;  // -1 automatic, 0 never, [NC*10000 +] W*100 + S always (slab shape)
+    int graph_mode = -1;  // golhip_set_graphs: -1 automatic, 0 never, 1 whenever the plan allows
+    // RCCL fail-fast (rank mode): every host wait on work that can depend on an RCCL transfer polls
+    // ncclCommGetAsyncError against a deadline and aborts the communicator when it passes
+    // (golhip_set_comm_timeout); the communicator is non-blocking, so no RCCL call blocks the host
+    int64_t comm_timeout_ms = 0;
+    double queued_s = 0.0;  // modelled seconds of stencil work queued since the last full sync
+    bool comm_failed = false;
+    // depth of the boundary bands the last split block ran on the edge stream (0: none, e.g. a strip
+    // shorter than 3K or a non-split launch): its rows [0, K) and [rows - K, rows) are exactly what
+    // the next exchange sends, so with K' <= edge_k that exchange waits only for those bands
+    int edge_k = 0;
+    std::string comm_pending;  // the last RCCL operation enqueued (rank, peers, K, bytes)
+    int test_recv_extra_rows = 0;  // GOLHIP_RING_SELF=2: the top-halo receive posts K + 1 rows
     std::vector<Shard> shards;
     int cur = 0;
     bool prev_valid = false;
@@ -158,12 +179,103 @@ int fail(golhip_t h, int code, const char *fmt, ...) {
                         "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
     } while (0)
 
-#define NCCLCHK(h, expr)                                                                    \
-    do {                                                                                    \
-        ncclResult_t r_ = (expr);                                                           \
-        if (r_ != ncclSuccess)                                                              \
-            return fail((h), GOLHIP_ERR_RCCL, "%s: %s (%s:%d)", #expr,                      \
-                        ncclGetErrorString(r_), __FILE__, __LINE__);                        \
+// ---- RCCL fail-fast --------------------------------------------------------------------------
+// True when device work of this handle can wait on an RCCL transfer (rank mode over RCCL: the
+// boundary bands wait for the halo event, the compute stream for the boundary bands, counts for
+// the all-reduce).  Only then do host waits poll; everything else synchronises directly.
+bool rccl_waits(golhip_t h) { return h->rank_mode && h->split && !h->host_comm_on; }
+
+// Abort the communicator (its kernels see the abort flag and return) and fail the call with the
+// pending operation named.  The handle stays unusable for device work afterwards (comm_failed).
+int comm_abort(golhip_t h, const char *why, ncclResult_t state) {
+    for (auto &s : h->shards)
+        if (s.comm_nccl) {
+            (void)ncclCommAbort(s.comm_nccl);
+            s.comm_nccl = nullptr;
+        }
+    h->comm_failed = true;
+    return fail(h, GOLHIP_ERR_RCCL, "rank %d of %d: %s: %s (communicator state: %s); communicator aborted",
+                h->shards.empty() ? -1 : h->shards[0].rank, h->world_size, why,
+                h->comm_pending.empty() ? "no RCCL operation pending" : h->comm_pending.c_str(),
+                ncclGetErrorString(state));
+}
+
+using Clock = std::chrono::steady_clock;
+// Deadline of a wait: the handle's timeout plus 10x the modelled time of the stencil work the host
+// queued since the last full sync (a long golhip_step of a big board is not a hang).
+int64_t wait_budget_ms(golhip_t h) {
+    return (int64_t)std::min((double)h->comm_timeout_ms + 10.0 * h->queued_s * 1e3, 3.6e6);
+}
+
+// Poll `done` (0 = finished, 1 = not yet, < 0 = error code already set) until it finishes, the
+// communicator reports an asynchronous error, or the deadline passes.
+template <class F>
+int poll_until(golhip_t h, const char *what, F &&done) {
+    const int64_t budget_ms = wait_budget_ms(h);
+    const Clock::time_point deadline = Clock::now() + std::chrono::milliseconds(budget_ms);
+    int spins = 0;
+    for (;;) {
+        const int r = done();
+        if (r <= 0) return r;
+        for (auto &s : h->shards) {
+            ncclResult_t st = ncclSuccess;
+            if (s.comm_nccl && ncclCommGetAsyncError(s.comm_nccl, &st) == ncclSuccess &&
+                st != ncclSuccess && st != ncclInProgress)
+                return comm_abort(h, what, st);
+        }
+        if (Clock::now() > deadline) {
+            ncclResult_t st = ncclInProgress;
+            if (!h->shards.empty() && h->shards[0].comm_nccl)
+                (void)ncclCommGetAsyncError(h->shards[0].comm_nccl, &st);
+            char buf[160];
+            std::snprintf(buf, sizeof buf, "%s did not complete within %lld ms", what,
+                          (long long)budget_ms);
+            return comm_abort(h, buf, st);
+        }
+        if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(spins > 4096 ? 200 : 20));
+    }
+}
+
+// hipStreamSynchronize, bounded by the RCCL deadline in rank mode.
+int wait_stream(golhip_t h, hipStream_t st) {
+    if (h->comm_failed)
+        return fail(h, GOLHIP_ERR_RCCL, "the communicator was aborted by an earlier failure: %s",
+                    h->comm_pending.c_str());
+    if (!rccl_waits(h)) {
+        const hipError_t e = hipStreamSynchronize(st);
+        if (e != hipSuccess)
+            return fail(h, GOLHIP_ERR_HIP, "hipStreamSynchronize: %s", hipGetErrorString(e));
+        return GOLHIP_OK;
+    }
+    return poll_until(h, "device work behind the RCCL transfers", [&]() -> int {
+        const hipError_t e = hipStreamQuery(st);
+        if (e == hipSuccess) return 0;
+        if (e == hipErrorNotReady) return 1;
+        return fail(h, GOLHIP_ERR_HIP, "hipStreamQuery: %s", hipGetErrorString(e));
+    });
+}
+
+// After a non-blocking RCCL call: wait until the communicator has finished setting it up
+// (ncclInProgress -> ncclSuccess) before the next RCCL call, bounded by the deadline.
+int comm_ready(golhip_t h, ncclComm_t c, const char *what) {
+    return poll_until(h, what, [&]() -> int {
+        ncclResult_t st = ncclSuccess;
+        if (ncclCommGetAsyncError(c, &st) != ncclSuccess) return 0;
+        return st == ncclInProgress ? 1 : 0;  // errors are taken by poll_until
+    });
+}
+
+#define SYNCCHK(h, stream)                      \
+    do {                                        \
+        int rc_ = wait_stream((h), (stream));   \
+        if (rc_) return rc_;                    \
+    } while (0)
+
+// An RCCL call on a non-blocking communicator: ncclInProgress is not an error (comm_ready waits).
+#define NCCLCALL(h, what, expr)                                                                   \
+    do {                                                                                          \
+        ncclResult_t r_ = (expr);                                                                 \
+        if (r_ != ncclSuccess && r_ != ncclInProgress) return comm_abort((h), (what), r_);        \
     } while (0)
 
 int64_t lcm64(int64_t a, int64_t b) { return a / std::gcd(a, b) * b; }
@@ -189,7 +301,7 @@ int check_device_arch(golhip_t h, int device) {
 int ensure_extract_scratch(golhip_t h, Shard &s, int64_t rows, int64_t slots) {
     if (rows <= s.ex_rows_cap && slots <= s.ex_slots_cap) return GOLHIP_OK;
     HIPCHK(h, hipSetDevice(s.device));
-    HIPCHK(h, hipStreamSynchronize(s.compute));
+    SYNCCHK(h, s.compute);
     if (!s.ex_block_sums)
         HIPCHK(h, hipMalloc(&s.ex_block_sums, sizeof(unsigned long long) * golhip::kScanBlocks));
     if (rows > s.ex_rows_cap) {
@@ -235,18 +347,43 @@ int alloc_shard(golhip_t h, Shard &s) {
     // (GOLHIP_STAGE_BYTES, read at create, shrinks it: tests force multi-chunk transfers)
     int64_t cap = kStageBytes;
     if (const char *e = std::getenv("GOLHIP_STAGE_BYTES")) cap = std::max<int64_t>(1, std::atoll(e));
-    s.stage_bytes = std::max<int64_t>(h->width, std::min<int64_t>(cap, s.rows * h->width));
+    // at least one row of every transfer unit: a byte row (width bytes) and a uint64 word row
+    // (8 * ceil(width / 64) bytes, larger than a byte row for widths below 8)
+    const int64_t row_unit = std::max<int64_t>(h->width, 8 * ((h->width + 63) / 64));
+    s.stage_bytes = std::max<int64_t>(row_unit, std::min<int64_t>(cap, s.rows * h->width));
     HIPCHK(h, hipMalloc(&s.stage, (size_t)s.stage_bytes));
-    HIPCHK(h, hipStreamSynchronize(s.compute));
+    SYNCCHK(h, s.compute);
     return ensure_extract_scratch(h, s, s.rows, 1);
 }
 
-void free_shard(Shard &s) {
+// drain_ms > 0 (a handle whose work can wait on RCCL): wait at most that long for the streams; a
+// stream still busy after it (an RCCL transfer nothing will ever match) is left to the process's
+// teardown, and its memory is not freed under it.
+void free_shard(Shard &s, int64_t drain_ms = 0) {
     (void)hipSetDevice(s.device);
-    if (s.compute) (void)hipStreamSynchronize(s.compute);
-    if (s.comm) (void)hipStreamSynchronize(s.comm);
-    if (s.edge) (void)hipStreamSynchronize(s.edge);
-    if (s.comm_nccl) (void)ncclCommDestroy(s.comm_nccl);
+    bool drained = true;
+    for (hipStream_t st : {s.compute, s.comm, s.edge}) {
+        if (!st) continue;
+        if (drain_ms <= 0) {
+            (void)hipStreamSynchronize(st);
+            continue;
+        }
+        const Clock::time_point end = Clock::now() + std::chrono::milliseconds(drain_ms);
+        hipError_t e;
+        while ((e = hipStreamQuery(st)) == hipErrorNotReady && Clock::now() < end)
+            std::this_thread::sleep_for(std::chrono::microseconds(200));
+        drained = drained && e != hipErrorNotReady;
+    }
+    if (s.comm_nccl) {
+        if (drained)
+            (void)ncclCommDestroy(s.comm_nccl);
+        else
+            (void)ncclCommAbort(s.comm_nccl);
+    }
+    if (!drained) {
+        s = Shard{};
+        return;
+    }
     for (auto &b : s.buf)
         if (b) (void)hipFree(b);
     if (s.slots) (void)hipFree(s.slots);
@@ -299,11 +436,18 @@ int setup_engine(golhip_t h, int width, int height, int world, int k) {
     h->k = k;
     h->split = world > 1;
     h->halo = h->split ? k : 0;
+    h->count_window = kCountWindowDefault;
+    h->comm_timeout_ms = g_comm_timeout_ms.load();
+#ifdef GOLHIP_TUNING
+    // The tuning build's selectors (read at create).  The production library reads none of them:
+    // a stray variable cannot change its kernels (the setters below are the explicit interface).
     if (const char *e = std::getenv("GOLHIP_BAND_ROWS")) h->band_rows = std::atoi(e);
     // measurement knob (scripts/pmc_passes.sh): every bulk launch exactly k deep, as
     // golhip_set_fixed_k(h, 1) -- the planner would otherwise run its fastest depth <= k
     if (const char *e = std::getenv("GOLHIP_FIXED_K")) h->fixed_k = std::atoi(e) != 0;
-    h->count_window = count_window_env();
+    if (const char *e = std::getenv("GOLHIP_COUNT_WINDOW"))
+        h->count_window = std::max(kCountWindowMin, std::atoi(e));
+    if (const char *e = std::getenv("GOLHIP_GRAPHS")) h->graph_mode = std::atoi(e) != 0;
     if (const char *e = std::getenv("GOLHIP_SPLIT")) h->force_split = std::atoi(e);
     if (const char *e = std::getenv("GOLHIP_TILE")) h->force_tile = std::atoi(e);
     if (const char *e = std::getenv("GOLHIP_SLAB")) h->force_slab = std::atoi(e);
@@ -323,6 +467,7 @@ int setup_engine(golhip_t h, int width, int height, int world, int k) {
                      : std::strcmp(e, "pre63") == 0 ? golhip::kVariantPre63
                      : std::strcmp(e, "prodmask") == 0 ? golhip::kVariantProdMask
                                                        : golhip::kVariantProd;  // prod
+#endif
     return GOLHIP_OK;
 }
 
@@ -692,6 +837,15 @@ int timing_collect(golhip_t h) {
     if (h->tused == 0) return GOLHIP_OK;
     HIPCHK(h, hipSetDevice(h->shards[0].device));
     for (size_t i = 0; i < h->tused; ++i) {
+        if (rccl_waits(h)) {
+            const hipEvent_t ev = h->tpool[i].b;
+            int rc = poll_until(h, "a timed launch behind the RCCL transfers", [&]() -> int {
+                const hipError_t e = hipEventQuery(ev);
+                return e == hipSuccess ? 0 : e == hipErrorNotReady ? 1 : fail(h, GOLHIP_ERR_HIP,
+                    "hipEventQuery: %s", hipGetErrorString(e));
+            });
+            if (rc) return rc;
+        }
         HIPCHK(h, hipEventSynchronize(h->tpool[i].b));
         float ms = 0.f;
         HIPCHK(h, hipEventElapsedTime(&ms, h->tpool[i].a, h->tpool[i].b));
@@ -734,7 +888,7 @@ int exchange_halos(golhip_t h, int K) {
             if (plan[i].kind == 0)
                 HIPCHK(h, hipMemcpyAsync(h->hc_buf[i], r0 + plan[i].row * h->pitch, bytes,
                                          hipMemcpyDeviceToHost, s.compute));
-        HIPCHK(h, hipStreamSynchronize(s.compute));
+        SYNCCHK(h, s.compute);
         if (h->host_comm.exchange(h->host_comm.ctx, plan, 4, h->hc_buf, bytes) != 0)
             return fail(h, GOLHIP_ERR_RCCL, "host transport: exchange of %d-row halos failed", K);
         for (int i = 0; i < 4; ++i)
@@ -742,27 +896,57 @@ int exchange_halos(golhip_t h, int K) {
                 HIPCHK(h, hipMemcpyAsync(r0 + plan[i].row * h->pitch, h->hc_buf[i], bytes,
                                          hipMemcpyHostToDevice, s.comm));
     } else if (h->rank_mode) {
-        for (auto &s : h->shards) HIPCHK(h, hipStreamWaitEvent(s.comm, s.ev_ready, 0));
-        NCCLCHK(h, ncclGroupStart());
-        for (auto &s : h->shards) {
-            golhip_xfer plan[4];
-            halo_plan(h->world_size, s.rank, s.rows, K, plan);
-            uint32_t *r0 = h->row0(s, h->cur);
-            for (const golhip_xfer &x : plan) {
-                uint32_t *p = r0 + x.row * h->pitch;
-                if (x.kind == 0)
-                    NCCLCHK(h, ncclSend(p, bytes, ncclUint8, x.peer, s.comm_nccl, s.comm));
-                else
-                    NCCLCHK(h, ncclRecv(p, bytes, ncclUint8, x.peer, s.comm_nccl, s.comm));
+        if (h->comm_failed)
+            return fail(h, GOLHIP_ERR_RCCL, "the communicator was aborted by an earlier failure: %s",
+                        h->comm_pending.c_str());
+        // Early exchange: the rows this exchange sends are the last block's boundary bands (edge
+        // stream), done long before its interior -- so the transfer overlaps the previous block's
+        // interior and the boundary bands of this block find their halos already in place.  The
+        // halo rows it receives into were last read by the boundary bands two blocks back, which
+        // precede the last block's bands on the edge stream.  Otherwise (deeper K than those
+        // bands, no bands last block) it waits for the whole last block (ev_ready).
+        for (auto &s : h->shards)
+            HIPCHK(h, hipStreamWaitEvent(s.comm, K <= h->edge_k ? s.ev_edge : s.ev_ready, 0));
+        Shard &s = h->shards[0];  // rank mode: one strip per process
+        golhip_xfer plan[4];
+        halo_plan(h->world_size, s.rank, s.rows, K, plan);
+        // what a stuck exchange reports (golhip_last_error after ERR_RCCL)
+        char desc[256];
+        std::snprintf(desc, sizeof desc,
+                      "halo exchange of K = %d rows (%zu bytes per transfer): send rows [%lld, +%d) "
+                      "-> rank %d, rows [0, +%d) -> rank %d; receive rows [-%d, ...) <- rank %d, "
+                      "[%lld, ...) <- rank %d",
+                      K, bytes, (long long)(s.rows - K), K, plan[0].peer, K, plan[1].peer, K,
+                      plan[2].peer, (long long)s.rows, plan[3].peer);
+        h->comm_pending = desc;
+        uint32_t *r0 = h->row0(s, h->cur);
+        NCCLCALL(h, "ncclGroupStart", ncclGroupStart());
+        for (int i = 0; i < 4; ++i) {
+            const golhip_xfer &x = plan[i];
+            uint32_t *p = r0 + x.row * h->pitch;
+            if (x.kind == 0) {
+                NCCLCALL(h, "ncclSend", ncclSend(p, bytes, ncclUint8, x.peer, s.comm_nccl, s.comm));
+            } else {
+                // test hook (GOLHIP_RING_SELF=2): the top-halo receive (rows -K .. 0, in bounds)
+                // asks for one row more than the matching send delivers
+                const size_t rb = bytes + (i == 2 ? (size_t)h->test_recv_extra_rows * h->pitch * 4 : 0);
+                NCCLCALL(h, "ncclRecv", ncclRecv(p, rb, ncclUint8, x.peer, s.comm_nccl, s.comm));
             }
         }
-        NCCLCHK(h, ncclGroupEnd());
+        NCCLCALL(h, "ncclGroupEnd", ncclGroupEnd());
+        int rc = comm_ready(h, s.comm_nccl, "the halo exchange's RCCL group");
+        if (rc) return rc;
     } else {
         const int n = (int)h->shards.size();
         for (int i = 0; i < n; ++i) {
             Shard &s = h->shards[i];
             Shard &up = h->shards[(i - 1 + n) % n], &down = h->shards[(i + 1) % n];
             HIPCHK(h, hipSetDevice(s.device));
+            // the neighbours read this strip's rows in THEIR comm streams: this strip's next block
+            // (which overwrites the buffer they read, the interior rows included when K shrinks)
+            // waits for their previous copies (ev_halo still marks them), then for its own ones
+            HIPCHK(h, hipStreamWaitEvent(s.compute, up.ev_halo, 0));
+            HIPCHK(h, hipStreamWaitEvent(s.compute, down.ev_halo, 0));
             HIPCHK(h, hipStreamWaitEvent(s.comm, up.ev_ready, 0));
             HIPCHK(h, hipStreamWaitEvent(s.comm, down.ev_ready, 0));
             uint32_t *r0 = h->row0(s, h->cur);
@@ -821,7 +1005,9 @@ int step_block(golhip_t h, int K, int64_t slot_gen, int64_t diff_slot = kDiffNon
             HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, pb, slots, s.edge));
             HIPCHK(h, hipEventRecord(s.ev_edge, s.edge));
             HIPCHK(h, hipStreamWaitEvent(s.compute, s.ev_edge, 0));
+            h->edge_k = K;
         } else {
+            h->edge_k = 0;
             HIPCHK(h, hipStreamWaitEvent(s.compute, s.ev_halo, 0));
             StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0, 0, slots != nullptr);
             p.diff = diff;
@@ -831,6 +1017,10 @@ int step_block(golhip_t h, int K, int64_t slot_gen, int64_t diff_slot = kDiffNon
     if (h->timing) {
         h->tlaunches += 1;
         h->tgens += K;
+    }
+    {  // the wait deadline's allowance for queued work (rank mode, poll_until)
+        const double cells = (double)h->L * (double)plan_rows(h);
+        h->queued_s += cells * K / (launch_rate_tcups(K, cells) * 1e12) + kLaunchOverheadUs * 1e-6;
     }
     h->cur = nxt;
     h->turn += K;
@@ -868,21 +1058,31 @@ int flush_counts_window(golhip_t h, int n, int64_t off) {
 int sync_all(golhip_t h) {
     for (auto &s : h->shards) {
         HIPCHK(h, hipSetDevice(s.device));
-        HIPCHK(h, hipStreamSynchronize(s.comm));
-        HIPCHK(h, hipStreamSynchronize(s.edge));
-        HIPCHK(h, hipStreamSynchronize(s.compute));
+        SYNCCHK(h, s.comm);
+        SYNCCHK(h, s.edge);
+        SYNCCHK(h, s.compute);
     }
+    h->queued_s = 0.0;
     return GOLHIP_OK;
 }
 
 // Sum n uint64 device values over every strip of the board into host memory `out`:
 // strips of this process are summed on the host, ranks with one ncclAllReduce.
 int reduce_u64(golhip_t h, const std::vector<unsigned long long *> &bufs, size_t n, uint64_t *out) {
-    if (h->rank_mode && h->split && !h->host_comm_on) {
+    if (rccl_waits(h)) {
         Shard &s = h->shards[0];
+        if (h->comm_failed)
+            return fail(h, GOLHIP_ERR_RCCL, "the communicator was aborted by an earlier failure: %s",
+                        h->comm_pending.c_str());
         HIPCHK(h, hipSetDevice(s.device));
-        NCCLCHK(h, ncclAllReduce(bufs[0], bufs[0], n, ncclUint64, ncclSum, s.comm_nccl,
-                                 s.compute));
+        char desc[128];
+        std::snprintf(desc, sizeof desc, "ncclAllReduce of %zu uint64 counts (%zu bytes) over %d ranks",
+                      n, n * sizeof(uint64_t), h->world_size);
+        h->comm_pending = desc;
+        NCCLCALL(h, "ncclAllReduce", ncclAllReduce(bufs[0], bufs[0], n, ncclUint64, ncclSum,
+                                                   s.comm_nccl, s.compute));
+        int rc = comm_ready(h, s.comm_nccl, "the count all-reduce");
+        if (rc) return rc;
     }
     std::vector<uint64_t> tmp(n);
     for (size_t i = 0; i < h->shards.size(); ++i) {
@@ -890,7 +1090,7 @@ int reduce_u64(golhip_t h, const std::vector<unsigned long long *> &bufs, size_t
         HIPCHK(h, hipSetDevice(s.device));
         HIPCHK(h, hipMemcpyAsync(i == 0 ? out : tmp.data(), bufs[i], n * sizeof(uint64_t),
                                  hipMemcpyDeviceToHost, s.compute));
-        HIPCHK(h, hipStreamSynchronize(s.compute));
+        SYNCCHK(h, s.compute);
         if (i > 0)
             for (size_t j = 0; j < n; ++j) out[j] += tmp[j];
     }
@@ -929,7 +1129,7 @@ int extract_cells(golhip_t h, const std::vector<const uint32_t *> &a,
     std::vector<size_t> shard_total(ns, 0);
     for (size_t i = 0; i < ns; ++i) {
         HIPCHK(h, hipSetDevice(h->shards[i].device));
-        HIPCHK(h, hipStreamSynchronize(h->shards[i].compute));
+        SYNCCHK(h, h->shards[i].compute);
         for (int64_t t = 0; t < slots; ++t) shard_total[i] += cnt[i][t];
         total += shard_total[i];
     }
@@ -953,7 +1153,7 @@ int extract_cells(golhip_t h, const std::vector<const uint32_t *> &a,
         if (shard_total[i] == 0) continue;
         HIPCHK(h, hipSetDevice(s.device));
         if (shard_total[i] > s.ex_xy_cap) {  // grow the device list (rare: a longer list)
-            HIPCHK(h, hipStreamSynchronize(s.compute));
+            SYNCCHK(h, s.compute);
             if (s.ex_xy) HIPCHK(h, hipFree(s.ex_xy));
             s.ex_xy = nullptr;
             const size_t want = std::max(shard_total[i], s.ex_xy_cap * 2);
@@ -1008,7 +1208,7 @@ int transfer_bytes(golhip_t h, uint8_t *host, size_t row_stride, bool to_device)
                                            stage, (size_t)W, (size_t)W, (size_t)nr,
                                            hipMemcpyDeviceToHost, s.compute));
             }
-            HIPCHK(h, hipStreamSynchronize(s.compute));
+            SYNCCHK(h, s.compute);
         }
         hrow += s.rows;
     }
@@ -1022,7 +1222,7 @@ int create_common(golhip_t h) {
         // each launch depth is its own code object, loaded at its first launch (~1 ms): load them
         // all now, not inside the first timed or latency-sensitive step
         HIPCHK(h, golhip::warm_stencils(h->variant, s.compute));
-        HIPCHK(h, hipStreamSynchronize(s.compute));
+        SYNCCHK(h, s.compute);
     }
     return GOLHIP_OK;
 }
@@ -1037,7 +1237,7 @@ constexpr int kGraphGensBig = 4096;
 bool small_board(double cells, int K) { return cells * K <= 8e9; }
 bool graph_worthy(golhip_t h, int K) {
     if (h->split || h->shards.size() != 1) return false;
-    if (const char *e = std::getenv("GOLHIP_GRAPHS")) return std::atoi(e) != 0;
+    if (h->graph_mode >= 0) return h->graph_mode != 0;  // golhip_set_graphs
     return small_board((double)h->L * (double)h->height, K);
 }
 
@@ -1084,7 +1284,8 @@ int graph_for(golhip_t h, int K, int M, bool counting, hipGraphExec_t *out) {
     Shard &s = h->shards[0];
     const int64_t band = auto_band(h, s.rows, K, 0, counting);
     for (auto &g : h->graphs)
-        if (g.K == K && g.M == M && g.cur == h->cur && g.counting == counting && g.band == band) {
+        if (g.K == K && g.M == M && g.cur == h->cur && g.counting == counting && g.band == band &&
+            g.tail_bands == h->tail_bands && g.tail_rows == h->tail_rows) {
             *out = g.exec;
             return GOLHIP_OK;
         }
@@ -1112,6 +1313,8 @@ int graph_for(golhip_t h, int K, int M, bool counting, hipGraphExec_t *out) {
     g.cur = h->cur;
     g.counting = counting;
     g.band = band;
+    g.tail_bands = h->tail_bands;
+    g.tail_rows = h->tail_rows;
     err = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
     (void)hipGraphDestroy(graph);
     if (err != hipSuccess) return fail(h, GOLHIP_ERR_HIP, "graph instantiate: %s", hipGetErrorString(err));
@@ -1239,10 +1442,13 @@ int golhip_create_rank(int width, int height, int rank, int world_size, int devi
     h->rank_mode = true;
     // Test hook: GOLHIP_RING_SELF=1 makes a world-1 rank engine a ring of ONE halo'd strip whose
     // halos go through RCCL send/recv to itself, so the whole rank-mode path (plan, RCCL group,
-    // interior/boundary overlap, count all-reduce) runs on a one-GPU box.
+    // interior/boundary overlap, count all-reduce) runs on a one-GPU box.  GOLHIP_RING_SELF=2:
+    // the same ring, whose top-halo receive asks for one row more than the matching send delivers
+    // -- an exchange that cannot complete as posted, for the fail-fast test (tests/test_gpu_failfast.py).
     if (ring_self) {
         h->split = true;
         h->halo = k;
+        h->test_recv_extra_rows = std::atoi(rs) == 2 ? 1 : 0;
     }
     h->shards.resize(1);
     Shard &s = h->shards[0];
@@ -1260,18 +1466,30 @@ int golhip_create_rank(int width, int height, int rank, int world_size, int devi
             goto fail;
         }
         (void)hipSetDevice(device);
-        const ncclResult_t nr = ncclCommInitRank(&s.comm_nccl, world_size, id, rank);
-        if (nr != ncclSuccess) {
-            rc = fail(h, GOLHIP_ERR_RCCL, "ncclCommInitRank(rank %d of %d, device %d): %s", rank,
-                      world_size, device, ncclGetErrorString(nr));
+        // non-blocking communicator: no RCCL call blocks the host, every wait on one is bounded
+        // (poll_until); a rank whose peers never join fails here after the timeout
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = 0;
+        char desc[128];
+        std::snprintf(desc, sizeof desc, "ncclCommInitRankConfig(rank %d of %d, device %d)", rank,
+                      world_size, device);
+        h->comm_pending = desc;
+        const ncclResult_t nr = ncclCommInitRankConfig(&s.comm_nccl, world_size, id, rank, &cfg);
+        if (nr != ncclSuccess && nr != ncclInProgress) {
+            if (s.comm_nccl) (void)ncclCommAbort(s.comm_nccl);
+            s.comm_nccl = nullptr;
+            rc = fail(h, GOLHIP_ERR_RCCL, "%s: %s", desc, ncclGetErrorString(nr));
             goto fail;
         }
+        if ((rc = comm_ready(h, s.comm_nccl, "the communicator's set-up (waiting for every rank)")))
+            goto fail;
+        h->comm_pending.clear();
     }
     *out = h;
     return GOLHIP_OK;
 fail:
     g_create_error = h->err.empty() ? golhip_strerror(rc) : h->err;
-    for (auto &sh : h->shards) free_shard(sh);
+    for (auto &sh : h->shards) free_shard(sh, h->comm_timeout_ms);
     delete h;
     return rc;
 }
@@ -1329,7 +1547,7 @@ int golhip_destroy(golhip_t h) {
         (void)hipEventDestroy(tp.a);
         (void)hipEventDestroy(tp.b);
     }
-    for (auto &s : h->shards) free_shard(s);
+    for (auto &s : h->shards) free_shard(s, rccl_waits(h) ? h->comm_timeout_ms : 0);
     for (void *b : h->hc_buf)
         if (b) (void)hipHostFree(b);
     delete h;
@@ -1406,7 +1624,7 @@ int golhip_store_words(golhip_t h, uint64_t *out) {
                                                h->width, d, s.compute));
             HIPCHK(h, hipMemcpyAsync(out + (hrow + y) * wpr, d, sizeof(uint64_t) * (size_t)(nr * wpr),
                                      hipMemcpyDeviceToHost, s.compute));
-            HIPCHK(h, hipStreamSynchronize(s.compute));
+            SYNCCHK(h, s.compute);
         }
         hrow += s.rows;
     }
@@ -1430,7 +1648,7 @@ int golhip_load_words(golhip_t h, const uint64_t *in) {
                                      hipMemcpyHostToDevice, s.compute));
             HIPCHK(h, golhip::launch_words_in(d, nr, h->width, h->wd, h->row0(s, h->cur) + y * h->pitch,
                                               h->pitch, s.compute));
-            HIPCHK(h, hipStreamSynchronize(s.compute));
+            SYNCCHK(h, s.compute);
         }
         hrow += s.rows;
     }
@@ -1448,14 +1666,14 @@ static int run_steps(golhip_t h, int64_t turns, uint64_t *alive_per_turn, bool r
     if (turns == 0) return GOLHIP_OK;
     if ((ring || h->track_flips) && !variant_writes_flips(h->variant))
         return fail(h, GOLHIP_ERR_STATE,
-                    "flips need a production kernel variant (GOLHIP_VARIANT=%d cannot write them)",
+                    "flips need a production kernel variant (tuning variant %d cannot write them)",
                     h->variant);
     const bool counting = alive_per_turn != nullptr;
     if (counting) {
         for (auto &s : h->shards) {
             if (s.d_counts_cap < (size_t)turns) {
                 HIPCHK(h, hipSetDevice(s.device));
-                HIPCHK(h, hipStreamSynchronize(s.compute));
+                SYNCCHK(h, s.compute);
                 if (s.d_counts) HIPCHK(h, hipFree(s.d_counts));
                 s.d_counts = nullptr;
                 HIPCHK(h, hipMalloc(&s.d_counts, sizeof(unsigned long long) * (size_t)turns));
@@ -1574,7 +1792,7 @@ static int ensure_ring(golhip_t h, int64_t rc_cap) {
     if (h->ring_cap < rc_cap) {
         for (auto &s : h->shards) {
             HIPCHK(h, hipSetDevice(s.device));
-            HIPCHK(h, hipStreamSynchronize(s.compute));
+            SYNCCHK(h, s.compute);
             if (s.ring) HIPCHK(h, hipFree(s.ring));
             s.ring = nullptr;
             HIPCHK(h, hipMalloc(&s.ring, sizeof(uint32_t) * (size_t)(rc_cap * s.rows * h->pitch)));
@@ -1631,7 +1849,7 @@ int extract_rows(golhip_t h, int64_t slots, uint16_t *x, size_t cap, size_t *n,
                                            s.ex_offsets, s.ex_block_sums, s.compute));
     HIPCHK(h, hipMemcpyAsync(row_offsets, s.ex_offsets, sizeof(uint64_t) * (size_t)(rows + 1),
                              hipMemcpyDeviceToHost, s.compute));
-    HIPCHK(h, hipStreamSynchronize(s.compute));
+    SYNCCHK(h, s.compute);
     const size_t total = (size_t)row_offsets[rows];
     *n = total;
     if (total > cap) return fail(h, GOLHIP_ERR_CAP, "%zu cells do not fit in cap %zu", total, cap);
@@ -1648,7 +1866,7 @@ int extract_rows(golhip_t h, int64_t slots, uint16_t *x, size_t cap, size_t *n,
     HIPCHK(h, golhip::launch_extract_emit_x16(s.ring, nullptr, h->pitch, rows, h->width, s.ex_offsets,
                                               dx, total, s.compute));
     HIPCHK(h, hipMemcpyAsync(x, dx, sizeof(uint16_t) * total, hipMemcpyDeviceToHost, s.compute));
-    HIPCHK(h, hipStreamSynchronize(s.compute));
+    SYNCCHK(h, s.compute);
     return GOLHIP_OK;
 }
 
@@ -1695,7 +1913,7 @@ int golhip_track_flips(golhip_t h, int enable) {
     if (!h) return GOLHIP_ERR_ARG;
     if (enable && !variant_writes_flips(h->variant))
         return fail(h, GOLHIP_ERR_STATE,
-                    "flips need a production kernel variant (GOLHIP_VARIANT=%d cannot write them)",
+                    "flips need a production kernel variant (tuning variant %d cannot write them)",
                     h->variant);
     h->track_flips = enable != 0;
     if (h->track_flips)
@@ -1756,7 +1974,7 @@ static int ckpt_rows(golhip_t h, Shard &s, int64_t y, int64_t nr, uint8_t *host,
         else
             HIPCHK(h, hipMemcpy2DAsync(host, (size_t)rb, dev, (size_t)h->pitch * 4, (size_t)rb,
                                        (size_t)nr, hipMemcpyDeviceToHost, s.compute));
-        HIPCHK(h, hipStreamSynchronize(s.compute));
+        SYNCCHK(h, s.compute);
         return GOLHIP_OK;
     }
     // the byte codec in row chunks through the shard's stage
@@ -1774,11 +1992,11 @@ static int ckpt_rows(golhip_t h, Shard &s, int64_t y, int64_t nr, uint8_t *host,
                     bytes[(size_t)(r * W + x)] = (hrows[r * rb + x / 8] >> (x % 8)) & 1 ? 255 : 0;
             HIPCHK(h, hipMemcpyAsync(stage, bytes.data(), nb, hipMemcpyHostToDevice, s.compute));
             HIPCHK(h, golhip::launch_pack(stage, n, W, h->wd, drows, h->pitch, s.compute));
-            HIPCHK(h, hipStreamSynchronize(s.compute));
+            SYNCCHK(h, s.compute);
         } else {
             HIPCHK(h, golhip::launch_unpack(drows, h->pitch, n, W, stage, s.compute));
             HIPCHK(h, hipMemcpyAsync(bytes.data(), stage, nb, hipMemcpyDeviceToHost, s.compute));
-            HIPCHK(h, hipStreamSynchronize(s.compute));
+            SYNCCHK(h, s.compute);
             std::memset(hrows, 0, (size_t)(n * rb));
             for (int64_t r = 0; r < n; ++r)
                 for (int64_t x = 0; x < W; ++x)
@@ -1997,6 +2215,43 @@ int golhip_set_fixed_k(golhip_t h, int fixed) {
 int golhip_set_band_rows(golhip_t h, int band_rows) {
     if (!h || band_rows < 0) return GOLHIP_ERR_ARG;
     h->band_rows = band_rows;
+    return GOLHIP_OK;
+}
+
+int golhip_set_graphs(golhip_t h, int mode) {
+    if (!h || mode < -1 || mode > 1) return GOLHIP_ERR_ARG;
+    h->graph_mode = mode;
+    return GOLHIP_OK;
+}
+
+int golhip_set_count_window(golhip_t h, int generations) {
+    if (!h || generations < kCountWindowMin) return GOLHIP_ERR_ARG;
+    if (generations == h->count_window) return GOLHIP_OK;
+    int rc = sync_all(h);
+    if (rc) return rc;
+    // the slots are zero between calls (every finalize re-zeroes what it summed); captured counting
+    // graphs bake the old slot array in, so they go
+    for (auto &g : h->graphs) (void)hipGraphExecDestroy(g.exec);
+    h->graphs.clear();
+    for (auto &s : h->shards) {
+        HIPCHK(h, hipSetDevice(s.device));
+        if (s.slots) HIPCHK(h, hipFree(s.slots));
+        s.slots = nullptr;
+        const size_t bytes = sizeof(unsigned long long) * (size_t)generations * golhip::kCountSlots;
+        HIPCHK(h, hipMalloc(&s.slots, bytes));
+        HIPCHK(h, hipMemsetAsync(s.slots, 0, bytes, s.compute));
+        SYNCCHK(h, s.compute);
+    }
+    h->count_window = generations;
+    return GOLHIP_OK;
+}
+
+int golhip_set_comm_timeout(golhip_t h, int64_t ms) {
+    if (ms <= 0) return GOLHIP_ERR_ARG;
+    if (h)
+        h->comm_timeout_ms = ms;
+    else
+        g_comm_timeout_ms.store(ms);
     return GOLHIP_OK;
 }
 

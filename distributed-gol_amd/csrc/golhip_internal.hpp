@@ -9,6 +9,22 @@
 
 namespace golhip {
 
+// Two builds of the same sources (Makefile):
+//   lib/libgolhip.so         production: only the kernels the automatic planner runs (the
+//                            production drift stencil at every depth, gol_step1, the production
+//                            register-slab shapes); no tuning environment variable is read;
+//   lib_tuning/libgolhip.so  -DGOLHIP_TUNING: also the measured-and-rejected stencil variants,
+//                            the level-split and register-tile kernels, the other slab shapes and
+//                            the environment selectors of the A/B scripts (GOLHIP_VARIANT,
+//                            GOLHIP_SPLIT/TILE/SLAB, GOLHIP_BAND_ROWS, GOLHIP_FIXED_K,
+//                            GOLHIP_LDS_PAD, GOLHIP_STEP1).  Tests of those kernels and the
+//                            tuning scripts load it explicitly.
+#ifdef GOLHIP_TUNING
+constexpr bool kTuningBuild = true;
+#else
+constexpr bool kTuningBuild = false;
+#endif
+
 // Device layout of one row strip (see DESIGN.md "Data layout in HBM"):
 //   torus width L = lcm(width, 128) bits, wd = L/32 uint32 words per row, LSB-first
 //   (bit b of word j is x = 32j+b; identical bytes to LSB-first uint64 words), rows
@@ -109,11 +125,15 @@ inline int chunk_words(int K, int variant, bool counting = false) {
 GOLHIP_STENCIL_DEPTHS(GOLHIP_X)
 #undef GOLHIP_X
 
-// Tuning knob (GOLHIP_LDS_PAD = bytes of unused dynamic LDS per block): caps the resident blocks
-// per CU, to measure the stencil's sensitivity to occupancy.  0 in production.
+// Tuning knob (GOLHIP_LDS_PAD = bytes of unused dynamic LDS per block, tuning build only): caps the
+// resident blocks per CU, to measure the stencil's sensitivity to occupancy.  0 in production.
 inline size_t lds_pad_bytes() {
+#ifdef GOLHIP_TUNING
     const char *e = std::getenv("GOLHIP_LDS_PAD");
     return e ? (size_t)std::atol(e) : (size_t)0;
+#else
+    return 0;
+#endif
 }
 
 // Launch the K-generation stencil (K in GOLHIP_STENCIL_DEPTHS). count_slots (nullable) receives

@@ -1040,15 +1040,6 @@ __global__ __launch_bounds__(64 * S) void gol_stencil_split(const uint32_t *__re
 template <int K, int D>
 constexpr bool kHalfHalo = D == 1 && K <= 16;  // keep in sync with chunk_words()
 
-// Tuning knob GOLHIP_STEP1 = P*10 + NT selects gol_step1's prefetch depth and cache policy
-// (read once; unset = the production configuration).
-inline int step1_config() {
-    static const int cfg = [] {
-        const char *e = std::getenv("GOLHIP_STEP1");
-        return e ? std::atoi(e) : 42;
-    }();
-    return cfg;
-}
 template <int P, int NT>
 hipError_t launch_step1_cfg(const uint32_t *in, uint32_t *out, const StencilParams &p,
                             unsigned long long *slots, hipStream_t s) {
@@ -1062,6 +1053,23 @@ hipError_t launch_step1_cfg(const uint32_t *in, uint32_t *out, const StencilPara
     else
         hipLaunchKernelGGL((gol_step1<false, P, NT>), dim3(blocks), dim3(256), 0, s, in, out, p, slots);
     return hipGetLastError();
+}
+// Production gol_step1: 4 rows in flight, non-temporal stores (profiles/r01_tune_step1.txt).
+#ifndef GOLHIP_TUNING
+inline hipError_t launch_step1(const uint32_t *in, uint32_t *out, const StencilParams &p,
+                               unsigned long long *slots, hipStream_t s) {
+    return launch_step1_cfg<4, 2>(in, out, p, slots, s);
+}
+inline const void *step1_fn() { return (const void *)gol_step1<false, 4, 2>; }
+#else
+// Tuning build: GOLHIP_STEP1 = P*10 + NT selects the prefetch depth and cache policy (read once;
+// unset = the production configuration).
+inline int step1_config() {
+    static const int cfg = [] {
+        const char *e = std::getenv("GOLHIP_STEP1");
+        return e ? std::atoi(e) : 42;
+    }();
+    return cfg;
 }
 #define GOLHIP_STEP1_CONFIGS(X) \
     X(20, 2, 0) X(22, 2, 2) X(30, 3, 0) X(32, 3, 2) X(40, 4, 0) X(41, 4, 1) X(42, 4, 2) \
@@ -1085,6 +1093,7 @@ inline const void *step1_fn() {
         default: return (const void *)gol_step1<false, 4, 2>;
     }
 }
+#endif
 
 template <int K, bool SKEW, int D, int PF = 0, bool DR = false, int ZIP = 1, bool HH = kHalfHalo<K, D>,
           bool FILLU = true, bool ALLOW_LD = false, bool PRE = false, bool MASK = false>
@@ -1116,6 +1125,38 @@ hipError_t launch_stencil_k(const uint32_t *in, uint32_t *out, const StencilPara
     return hipGetLastError();
 }
 
+// The production kernel of depth K (kVariantProd): gol_step1 at K = 1; the drifting-sum stencil
+// with the column geometry measured fastest per depth and counting mode (prod_pre, internal.hpp).
+template <int K>
+hipError_t launch_prod(const uint32_t *in, uint32_t *out, const StencilParams &p,
+                       unsigned long long *slots, hipStream_t s) {
+    if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
+    else if constexpr (K <= 16) {
+        if (prod_pre(K, slots != nullptr))
+            return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true, true>(in, out, p, slots, s);
+        return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true>(in, out, p, slots, s);
+    } else return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true>(in, out, p, slots, s);
+}
+template <int K>
+const void *prod_fn() {
+    if constexpr (K == 1) return step1_fn();
+    else if constexpr (prod_pre(K)) return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1, true, false, 0, true>;
+    else return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1>;
+}
+
+#ifndef GOLHIP_TUNING
+// Production build: the production kernel whatever the handle's variant (always kVariantProd there).
+template <int K>
+hipError_t launch_variant(int, const uint32_t *in, uint32_t *out, const StencilParams &p,
+                          unsigned long long *slots, hipStream_t s) {
+    return launch_prod<K>(in, out, p, slots, s);
+}
+template <int K>
+const void *variant_fn(int) {
+    return prod_fn<K>();
+}
+#else
+// Tuning build: every measured variant (GOLHIP_VARIANT, tests/test_gpu_tuning.py, scripts/ab_*.py).
 template <int K>
 hipError_t launch_variant(int variant, const uint32_t *in, uint32_t *out, const StencilParams &p,
                           unsigned long long *slots, hipStream_t s) {
@@ -1137,12 +1178,7 @@ hipError_t launch_variant(int variant, const uint32_t *in, uint32_t *out, const 
             if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
             else return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true>(in, out, p, slots, s);
         case kVariantProd:  // per depth and counting: the fastest measured (golhip_internal.hpp)
-            if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
-            else if constexpr (K <= 16) {
-                if (prod_pre(K, slots != nullptr))
-                    return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true, true>(in, out, p, slots, s);
-                return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true>(in, out, p, slots, s);
-            } else return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true>(in, out, p, slots, s);
+            return launch_prod<K>(in, out, p, slots, s);
         case kVariantDriftNoFill:
             if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
             else return launch_stencil_k<K, false, 1, 1, (K <= 16), 1, kHalfHalo<K, 1>, false>(in, out, p, slots, s);
@@ -1182,10 +1218,7 @@ const void *variant_fn(int variant) {
         case kVariantDrift62:
             if constexpr (K == 1) return step1_fn();
             else return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1>;
-        case kVariantProd:
-            if constexpr (K == 1) return step1_fn();
-            else if constexpr (prod_pre(K)) return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1, true, false, 0, true>;
-            else return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1>;
+        case kVariantProd: return prod_fn<K>();
         case kVariantDriftNoFill:
             if constexpr (K == 1) return step1_fn();
             else return (const void *)gol_stencil<K, false, false, 1, 1, kHalfHalo<K, 1>, (K <= 16), 1, false>;
@@ -1203,6 +1236,7 @@ const void *variant_fn(int variant) {
         default: return (const void *)gol_stencil<K, false, true, 1, 0, kHalfHalo<K, 1>>;
     }
 }
+#endif  // GOLHIP_TUNING
 
 template <int K, int S>
 hipError_t launch_split_ks(const uint32_t *in, uint32_t *out, const StencilParams &p,

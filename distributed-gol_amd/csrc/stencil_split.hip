@@ -1,8 +1,12 @@
-// stencil_split.hip -- the level-split stencil (small boards) launchers.
+// stencil_split.hip -- the level-split stencil (gol_stencil_split) launchers.  Tuning build only:
+// since the register slab (stencil_tile.hip) took the small boards, the automatic planner never
+// picks the level split (pick_split needs fewer minimal-band waves than the slab leaves it), so the
+// production library compiles no instantiation and reports every (K, S) unsupported.
 #include "golhip_stencil.hpp"
 
 namespace golhip {
 
+#ifdef GOLHIP_TUNING
 bool stencil_split_supported(int K, int S) {
     if (S == 2) return K == 4 || K == 6 || K == 8 || K == 12 || K == 16 || K == 32;
     if (S == 4) return K == 4 || K == 8 || K == 12 || K == 16 || K == 32;
@@ -30,5 +34,15 @@ hipError_t warm_stencil_split(hipStream_t s) {
                        nullptr, p, nullptr);
     return hipGetLastError();
 }
+#else
+bool stencil_split_supported(int, int) { return false; }
+
+hipError_t launch_stencil_split(int, int, const uint32_t *, uint32_t *, const StencilParams &,
+                                unsigned long long *, hipStream_t) {
+    return hipErrorInvalidValue;
+}
+
+hipError_t warm_stencil_split(hipStream_t) { return hipSuccess; }
+#endif
 
 }  // namespace golhip

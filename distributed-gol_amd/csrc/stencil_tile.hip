@@ -579,6 +579,201 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
     }
 }
 
+// gol_slab2: gol_slab with the edge-row hand-off taken OFF the critical path.  gol_slab's waves
+// wait at each generation's barrier, then read their neighbours' edge-row sums from LDS, then
+// update their rows in NC rolling segments: the barrier and the LDS round trip sit in front of
+// every generation's work, and two segments per wave leave a SIMD with two waves on it short of
+// independent instructions (PMC, configs[1] 5120^2: VALU active 31 % of the wave cycles, parked at
+// barrier/waitcnt 45 %, profiles/r04/).  Here a generation is:
+//   1. the 3-cell sums of ALL S own rows, op-major (S independent chains);
+//   2. publish the two edge rows' sums to LDS;
+//   3. the new cells of the S - 2 interior rows, op-major -- they need only the wave's own sums,
+//      so they run while the neighbours are still publishing;
+//   4. the barrier, the neighbours' edge sums from LDS, and the two edge rows.
+// Only step 4's short tail (an LDS read and two 7-op rules) waits on the other waves.
+template <int K, int W, int S, bool COUNT, int LD>
+__global__ __launch_bounds__(64 * W) void gol_slab2(const uint32_t *__restrict__ in,
+                                                    uint32_t *__restrict__ out, StencilParams p,
+                                                    unsigned long long *__restrict__ slots) {
+    constexpr int T = W * S - 2 * K;
+    static_assert(T >= 1 && K >= 2 && K <= 32 && W >= 2 && S >= 3, "slab geometry");
+    __shared__ uint32_t ex[2][W + 2][4][64];  // as gol_slab: wave w's block is ex[par][w + 1]
+    __shared__ uint32_t cnt_lds[COUNT ? K : 1][COUNT ? W : 1][64];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    // XCD-aware order (gol_slab): XCD b % 8 gets a contiguous range of slabs
+    const int64_t ngroups = p.nbands * (int64_t)p.nchunks;
+    const int64_t per_xcd = (ngroups + kXcds - 1) / kXcds;
+    const int64_t group = (int64_t)(blockIdx.x % kXcds) * per_xcd + blockIdx.x / kXcds;
+    if (group >= ngroups) return;  // whole workgroup
+    const int64_t chunk = group % p.nchunks;
+    const int64_t bandi = group / p.nchunks;
+    int ya, yb;
+    band_rows(p, bandi, ya, yb);
+    const int nrows = yb - ya;
+    const int colraw = (int)chunk * kTileChunkWords + lane - 1;
+    const int col = (colraw + p.wd) % p.wd;
+    const int rowbytes = (int)(p.pitch * 4);
+    uint32_t c[S + 2];  // rows 1..S of this wave (c[0], c[S + 1] unused)
+    c[0] = c[S + 1] = 0;
+    load_rows<1, S>(c, in, p, ya - K + w * S, col);
+    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+        out + (int64_t)ya * p.pitch, 0, nrows * rowbytes, kBufferRsrcWord3);
+    __amdgpu_buffer_rsrc_t drsrc = orsrc;
+    if constexpr (LD == 1)
+        drsrc = __builtin_amdgcn_make_buffer_rsrc(p.diff + (int64_t)ya * p.pitch, 0,
+                                                  nrows * rowbytes, kBufferRsrcWord3);
+    const LaneStore ls = lane_store<false>(lane, colraw, col, p.wd);
+    const bool count_lane = lane >= 2 && colraw <= p.wd;
+    const int o0 = w * S - K;  // output row of c[1]
+    if constexpr (COUNT)
+        for (int j = 0; j < K; ++j) cnt_lds[j][w][lane] = 0;
+    if (w == 0)
+        for (int par = 0; par < 2; ++par)
+            for (int i = 0; i < 4; ++i) ex[par][0][i][lane] = ex[par][W + 1][i][lane] = 0u;
+    uint32_t *const ex_base0 = &ex[0][w][0][lane];
+    constexpr int kExPar = (W + 2) * 4 * 64;
+    uint32_t *const cnt_my = &cnt_lds[0][w][lane];
+    auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    auto cnt_sum = [&](int j) {
+        uint32_t a = 0;
+#pragma unroll
+        for (int ww = 0; ww < W; ++ww) a += cnt_lds[j][ww][lane];
+        return count_lane ? a : 0u;
+    };
+    // with 2S <= K the two halo waves take turns flushing the generation that is complete after
+    // generation g's barrier (g - 2, 0-based), as gol_slab does
+    auto flush_after_barrier = [&](int g) {
+        if constexpr (COUNT && 2 * S <= K) {
+            if (g >= 2 && w == ((g & 1) ? W - 1 : 0)) {
+                uint32_t acc[1] = {cnt_sum(g - 2)};
+                flush_counts<1>(acc, g - 2, lane, group, slots);
+            }
+        }
+    };
+    const bool full = o0 >= 0 && o0 + S <= nrows;
+    const bool halo = o0 + S <= 0 || o0 >= nrows;
+    // generation g (1-based) of this wave's rows
+    auto gen = [&](auto last_c, auto full_c, auto cnt_c, int g) {
+        constexpr bool LAST = decltype(last_c)::value, FULL = decltype(full_c)::value;
+        constexpr bool CNT = COUNT && decltype(cnt_c)::value;
+        const int gi = g - 1;
+        uint32_t cnt = 0;
+        __amdgpu_buffer_rsrc_t grsrc = orsrc;
+        if constexpr (LD == 2)
+            grsrc = __builtin_amdgcn_make_buffer_rsrc(p.diff + gi * p.diff_stride + (int64_t)ya * p.pitch,
+                                                      0, nrows * rowbytes, kBufferRsrcWord3);
+        auto emit = [&](int r, uint32_t nx, uint32_t centre) {  // r: 1..S (compile time after unroll)
+            const int o = o0 + r - 1;
+            const bool mine = FULL || (o >= 0 && o < nrows);  // wave-uniform
+            if (CNT) cnt = bcnt_acc(mine ? nx : 0u, cnt);
+            if constexpr (LD == 2) {
+                Words<1> dv;
+                dv.w[0] = realign_drift_rt(nx ^ centre, gi);
+                golhip::store_row<1, false>(grsrc, ls, dv, mine ? o * rowbytes : kOutOfRange);
+            }
+            if constexpr (LAST) {
+                const int rowoff = mine ? o * rowbytes : kOutOfRange;
+                Words<1> v;
+                v.w[0] = realign_drift<K>(nx);
+                golhip::store_row<1, false>(orsrc, ls, v, rowoff);
+                if constexpr (LD == 1) {
+                    Words<1> dv;
+                    dv.w[0] = realign_drift<K>(nx ^ centre);
+                    golhip::store_row<1, false>(drsrc, ls, dv, rowoff);
+                }
+            }
+        };
+        // 1. sums of all S rows (independent chains, op-major)
+        uint32_t x[S], s[S], cy[S], ctr[S];
+#pragma unroll
+        for (int i = 0; i < S; ++i) x[i] = c[i + 1];
+        sums_om<S>(x, s, cy, ctr);
+        // 2. publish the edge rows' sums
+        uint32_t *const b = ex_base0 + (g & 1) * kExPar;  // block w (the upper neighbour's)
+        b[256] = s[0];
+        b[320] = cy[0];
+        b[384] = s[S - 1];
+        b[448] = cy[S - 1];
+        // 3. the interior rows 2..S-1 (c[2..S-1]) from the wave's own sums
+        {
+            constexpr int NI = S - 2;
+            uint32_t as[NI], acy[NI], ms[NI], mcy[NI], mc[NI], bs[NI], bcy[NI], nx[NI];
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                as[i] = s[i], acy[i] = cy[i];
+                ms[i] = s[i + 1], mcy[i] = cy[i + 1], mc[i] = ctr[i + 1];
+                bs[i] = s[i + 2], bcy[i] = cy[i + 2];
+            }
+            life_om<NI>(as, acy, ms, mcy, mc, bs, bcy, nx, AllRows{});
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                emit(i + 2, nx[i], mc[i]);
+                if constexpr (!LAST) c[i + 2] = nx[i];
+            }
+        }
+        // 4. the neighbours' edge sums, then the two edge rows
+        lds_barrier();
+        const uint32_t ts = b[128], tcy = b[192];  // the upper neighbour's last row
+        const uint32_t bts = b[512], btcy = b[576];  // the lower neighbour's first row
+        flush_after_barrier(g);
+        {
+            uint32_t as[2] = {ts, s[S - 2]}, acy[2] = {tcy, cy[S - 2]};
+            uint32_t ms[2] = {s[0], s[S - 1]}, mcy[2] = {cy[0], cy[S - 1]}, mc[2] = {ctr[0], ctr[S - 1]};
+            uint32_t bs[2] = {s[1], bts}, bcy[2] = {cy[1], btcy}, nx[2];
+            life_om<2>(as, acy, ms, mcy, mc, bs, bcy, nx, AllRows{});
+            emit(1, nx[0], mc[0]);
+            emit(S, nx[1], mc[1]);
+            if constexpr (!LAST) {
+                c[1] = nx[0];
+                c[S] = nx[1];
+            }
+        }
+        if constexpr (CNT) cnt_my[gi * (W * 64)] = cnt;
+    };
+    // a generation this wave sits out (all its rows dead): keep the barrier count
+    auto idle = [&](int g) {
+        lds_barrier();
+        flush_after_barrier(g);
+    };
+    using No = std::false_type;
+    using Yes = std::true_type;
+    if constexpr (LD == 2 || !COUNT) {
+#pragma clang loop unroll(disable)
+        for (int g = 1; g < K; ++g) gen(No{}, No{}, Yes{}, g);
+        gen(Yes{}, No{}, Yes{}, K);
+    } else if (halo) {
+        const int g_end = std::min(std::min(w * S + S, W * S - w * S), K);
+        int g = 1;
+#pragma clang loop unroll(disable)
+        for (; g < g_end; ++g) gen(No{}, No{}, No{}, g);
+#pragma clang loop unroll(disable)
+        for (; g <= K; ++g) idle(g);
+    } else if (full) {
+#pragma clang loop unroll(disable)
+        for (int g = 1; g < K; ++g) gen(No{}, Yes{}, Yes{}, g);
+        gen(Yes{}, Yes{}, Yes{}, K);
+    } else {
+#pragma clang loop unroll(disable)
+        for (int g = 1; g < K; ++g) gen(No{}, No{}, Yes{}, g);
+        gen(Yes{}, No{}, Yes{}, K);
+    }
+    if constexpr (COUNT) {  // the generations not flushed yet
+        lds_barrier();
+        if constexpr (2 * S <= K) {
+            if (w == ((K & 1) ? 0 : W - 1)) {
+                uint32_t acc[1] = {cnt_sum(K - 1)};
+                flush_counts<1>(acc, K - 1, lane, group, slots);
+            }
+        } else {
+            for (int j = w; j < K; j += W) {
+                uint32_t acc[1] = {cnt_sum(j)};
+                flush_counts<1>(acc, j, lane, group, slots);
+            }
+        }
+    }
+}
+
 template <int K, int T>
 hipError_t launch_tile_kt(const uint32_t *in, uint32_t *out, const StencilParams &p,
                           unsigned long long *slots, hipStream_t s) {
@@ -598,11 +793,14 @@ hipError_t launch_tile_kt(const uint32_t *in, uint32_t *out, const StencilParams
 }
 
 // The production slab shapes (pick_reg_kernel): only these instantiate the every-generation
-// flips variant (LD = 2).
+// flips variant (LD = 2).  NC = kSlab2 selects gol_slab2 (the edge hand-off off the critical path).
+constexpr int kSlab2 = 9;
+constexpr bool slab_prod_ws(int K, int W, int S) {
+    return (K == 16 && W == 8 && S == 12) || (K == 16 && W == 12 && S == 8) ||
+           (K == 16 && W == 12 && S == 7) || (K == 8 && W == 8 && S == 8) || (K == 12 && W == 8 && S == 8);
+}
 constexpr bool slab_prod_shape(int K, int W, int S, int NC) {
-    return (K == 16 && W == 8 && S == 12 && NC == 2) || (K == 16 && W == 12 && S == 8 && NC == 2) ||
-           (K == 16 && W == 12 && S == 7 && NC == 2) || (K == 8 && W == 8 && S == 8 && NC == 4) ||
-           (K == 12 && W == 8 && S == 8 && NC == 4);
+    return slab_prod_ws(K, W, S) && (NC == kSlab2 || (K == 16 ? NC == 2 : NC == 4));
 }
 
 template <int K, int W, int S, int NC>
@@ -611,6 +809,29 @@ hipError_t launch_slab_kws(const uint32_t *in, uint32_t *out, const StencilParam
     const int64_t ngroups = p.nbands * (int64_t)p.nchunks;
     const unsigned blocks = (unsigned)std::max<int64_t>(1, (ngroups + kXcds - 1) / kXcds * kXcds);
     const dim3 block(64 * W);
+    if constexpr (NC == kSlab2) {
+        if (p.diff && p.diff_stride > 0) {
+            if constexpr (slab_prod_shape(K, W, S, NC)) {
+                if (slots)
+                    hipLaunchKernelGGL((gol_slab2<K, W, S, true, 2>), dim3(blocks), block, 0, s, in, out, p, slots);
+                else
+                    hipLaunchKernelGGL((gol_slab2<K, W, S, false, 2>), dim3(blocks), block, 0, s, in, out, p, slots);
+                return hipGetLastError();
+            } else {
+                return hipErrorNotSupported;
+            }
+        }
+        const int ld = p.diff ? 1 : 0;
+        if (ld && slots)
+            hipLaunchKernelGGL((gol_slab2<K, W, S, true, 1>), dim3(blocks), block, 0, s, in, out, p, slots);
+        else if (ld)
+            hipLaunchKernelGGL((gol_slab2<K, W, S, false, 1>), dim3(blocks), block, 0, s, in, out, p, slots);
+        else if (slots)
+            hipLaunchKernelGGL((gol_slab2<K, W, S, true, 0>), dim3(blocks), block, 0, s, in, out, p, slots);
+        else
+            hipLaunchKernelGGL((gol_slab2<K, W, S, false, 0>), dim3(blocks), block, 0, s, in, out, p, slots);
+        return hipGetLastError();
+    }
     if (p.diff && p.diff_stride > 0) {
         if constexpr (slab_prod_shape(K, W, S, NC)) {
             if (slots)
@@ -637,12 +858,24 @@ hipError_t launch_slab_kws(const uint32_t *in, uint32_t *out, const StencilParam
 
 }  // namespace
 
-// (K, waves, rows per wave, interleaved row chains): the production shapes (pick_reg_kernel) and
-// the tuning neighbours kept measurable (profiles/r03/small_boards_r03.txt)
-#define GOLHIP_SLAB_CONFIGS(X) \
-    X(8, 8, 4, 4) X(8, 8, 8, 4) X(12, 8, 8, 4) X(16, 8, 8, 4) X(16, 8, 12, 4) X(16, 16, 8, 4) \
-    X(16, 8, 12, 2) X(16, 12, 8, 2) X(16, 12, 8, 4) X(16, 12, 7, 2) X(16, 10, 8, 2) X(16, 14, 6, 2) \
-    X(16, 16, 6, 2) X(16, 16, 5, 2)
+// (K, waves, rows per wave, interleaved row chains): the production shapes (pick_reg_kernel:
+// slab_prod_shape above) in both builds; the tuning build adds the neighbours kept measurable
+// (profiles/r02/small_boards.txt, profiles/r03/r03e_tune_slab.log) and the register-tile kernel.
+#define GOLHIP_SLAB_PROD_CONFIGS(X) \
+    X(8, 8, 8, 4) X(12, 8, 8, 4) X(16, 8, 12, 2) X(16, 12, 8, 2) X(16, 12, 7, 2)
+#ifdef GOLHIP_TUNING
+#define GOLHIP_SLAB_CONFIGS(X) GOLHIP_SLAB_PROD_CONFIGS(X) \
+    X(8, 8, 4, 4) X(16, 8, 8, 4) X(16, 8, 12, 4) X(16, 16, 8, 4) \
+    X(16, 12, 8, 4) X(16, 10, 8, 2) X(16, 14, 6, 2) X(16, 16, 6, 2) X(16, 16, 5, 2) \
+    X(16, 8, 12, 9) X(16, 12, 8, 9) X(16, 12, 7, 9) X(8, 8, 8, 9) X(12, 8, 8, 9) X(16, 16, 6, 9) \
+    X(16, 16, 5, 9) X(16, 10, 8, 9) X(16, 8, 8, 9) X(16, 12, 6, 9)
+#define GOLHIP_TILE_CONFIGS(X) \
+    X(2, 16) X(4, 8) X(4, 16) X(4, 32) X(6, 16) X(8, 8) X(8, 16) X(8, 32) X(10, 16) X(12, 8) \
+    X(12, 16) X(12, 32) X(14, 16) X(16, 8) X(16, 16) X(16, 32)
+#else
+#define GOLHIP_SLAB_CONFIGS(X) GOLHIP_SLAB_PROD_CONFIGS(X)
+#define GOLHIP_TILE_CONFIGS(X)
+#endif
 
 bool stencil_slab_flips_every_gen(int K, int W, int S, int NC) {
     return stencil_slab_supported(K, W, S, NC) && slab_prod_shape(K, W, S, NC);
@@ -666,15 +899,12 @@ hipError_t launch_stencil_slab(int K, int W, int S, int NC, const uint32_t *in_r
     return hipErrorInvalidValue;
 }
 
-#define GOLHIP_TILE_CONFIGS(X) \
-    X(2, 16) X(4, 8) X(4, 16) X(4, 32) X(6, 16) X(8, 8) X(8, 16) X(8, 32) X(10, 16) X(12, 8) \
-    X(12, 16) X(12, 32) X(14, 16) X(16, 8) X(16, 16) X(16, 32)
-
 bool stencil_tile_supported(int K, int T) {
 #define GOLHIP_X(KK, TT) \
     if (K == KK && T == TT) return true;
     GOLHIP_TILE_CONFIGS(GOLHIP_X)
 #undef GOLHIP_X
+    (void)K, (void)T;
     return false;
 }
 
@@ -684,15 +914,15 @@ hipError_t launch_stencil_tile(int K, int T, const uint32_t *in_row0, uint32_t *
     if (K == KK && T == TT) return launch_tile_kt<KK, TT>(in_row0, out_row0, p, slots, s);
     GOLHIP_TILE_CONFIGS(GOLHIP_X)
 #undef GOLHIP_X
+    (void)K, (void)T, (void)in_row0, (void)out_row0, (void)p, (void)slots, (void)s;
     return hipErrorInvalidValue;
 }
 
+// Load the register kernels' code object before anything is timed (an empty launch: nbands = 0).
 hipError_t warm_stencil_tile(hipStream_t s) {
     StencilParams p{};
     p.nchunks = 1;  // nbands = 0: every wave returns at once
-    hipLaunchKernelGGL((gol_tile<16, 16, false, false>), dim3(1), dim3(256), 0, s, nullptr, nullptr, p,
-                       nullptr);
-    hipLaunchKernelGGL((gol_slab<16, 16, 8, false, 0>), dim3(1), dim3(1024), 0, s, nullptr, nullptr, p,
+    hipLaunchKernelGGL((gol_slab<16, 8, 12, false, 0, 2>), dim3(1), dim3(512), 0, s, nullptr, nullptr, p,
                        nullptr);
     return hipGetLastError();
 }

@@ -24,6 +24,10 @@ except Exception:  # pragma: no cover - torch is optional for the binding itself
 
 HERE = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("GOLHIP_LIB", HERE / "lib" / "libgolhip.so"))
+# The tuning build of the same sources (-DGOLHIP_TUNING, distributed-gol_amd/Makefile): the
+# production kernels plus the measured-and-rejected variants, the level-split / register-tile
+# kernels and the A/B environment selectors.  Only tests of those kernels and tuning scripts load it.
+TUNING_LIB_PATH = HERE / "lib_tuning" / "libgolhip.so"
 
 OK = 0
 ERR_ARG, ERR_HIP, ERR_OOM, ERR_CAP, ERR_RCCL, ERR_NODEV, ERR_STATE = -1, -2, -3, -4, -5, -6, -7
@@ -40,6 +44,7 @@ EXPORTS = [
     "golhip_store_bytes", "golhip_store_words", "golhip_load_words", "golhip_step",
     "golhip_alive_count", "golhip_alive_cells", "golhip_flips", "golhip_turn",
     "golhip_set_turn", "golhip_set_k", "golhip_set_band_rows", "golhip_set_tail_bands", "golhip_sync", "golhip_timing",
+    "golhip_set_graphs", "golhip_set_count_window", "golhip_set_comm_timeout",
     "golhip_kernel_time", "golhip_launch_plan", "golhip_launch_kind", "golhip_launch_kind_counts", "golhip_set_fixed_k", "golhip_track_flips",
     "golhip_step_flips", "golhip_flips_ring_capacity", "golhip_flips_fetch",
     "golhip_step_flips_rows", "golhip_flips_fetch_rows",
@@ -126,15 +131,23 @@ class Info(ctypes.Structure):
 
 
 _lib = None
+_libs: dict[str, ctypes.CDLL] = {}
 
 
 def load_library(path: Path | str | None = None) -> ctypes.CDLL:
-    """Load libgolhip.so (raises if it was not built: no fallback)."""
+    """Load libgolhip.so (raises if it was not built: no fallback).  path=None: the default library
+    (GOLHIP_LIB, an alternative build for A/B experiments, else the in-tree production build);
+    another path loads that build beside it (its own handle namespace, RTLD_LOCAL)."""
     global _lib
-    if _lib is not None:
+    if path is None and _lib is not None:
         return _lib
     # GOLHIP_LIB: an alternative build of the same library (A/B experiments); default in-tree
     p = Path(path) if path else Path(os.environ.get("GOLHIP_LIB", str(LIB_PATH)))
+    key = str(p.resolve()) if p.exists() else str(p)
+    if key in _libs:
+        if path is None:
+            _lib = _libs[key]
+        return _libs[key]
     if not p.exists():
         raise GolHipError(ERR_NODEV, f"{p} not built (run __graft_entry__.build())")
     L = ctypes.CDLL(str(p))
@@ -185,6 +198,9 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
         "golhip_flips_fetch_rows": ([H, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
                                      ctypes.c_void_p], i32),
         "golhip_sync": ([H], i32),
+        "golhip_set_graphs": ([H, i32], i32),
+        "golhip_set_count_window": ([H, i32], i32),
+        "golhip_set_comm_timeout": ([H, i64], i32),
         "golhip_timing": ([H, i32], i32),
         "golhip_kernel_time": ([H, ctypes.POINTER(ctypes.c_double), i64p, i64p], i32),
         "golhip_launch_plan": ([i64, i64, i32, i32, i64, ctypes.c_void_p, ctypes.c_size_t,
@@ -197,8 +213,38 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
-    _lib = L
+    _libs[key] = L
+    if path is None:
+        _lib = L
     return L
+
+
+def tuning_library() -> ctypes.CDLL:
+    """The tuning build (lib_tuning/libgolhip.so): pass it as Engine(..., lib=tuning_library()) to
+    run a non-production kernel (GOLHIP_VARIANT / GOLHIP_SPLIT / GOLHIP_TILE / GOLHIP_SLAB ...)."""
+    return load_library(TUNING_LIB_PATH)
+
+
+def set_default_comm_timeout(ms: int, lib: ctypes.CDLL | None = None) -> None:
+    """golhip_set_comm_timeout(NULL, ms): the RCCL deadline of engines created from now on."""
+    rc = (lib or load_library()).golhip_set_comm_timeout(None, int(ms))
+    if rc != OK:
+        raise GolHipError(rc, "set_comm_timeout: invalid argument")
+
+
+class _CallLog:
+    """The library seen through an engine: records the name of the last C ABI function called
+    (Engine.last_call), so a failed or stuck multi-rank run can say where it was."""
+
+    def __init__(self, lib: ctypes.CDLL, owner: "Engine"):
+        self._lib, self._owner = lib, owner
+
+    _QUIET = ("golhip_last_error", "golhip_strerror", "golhip_get_info")
+
+    def __getattr__(self, name):
+        if name not in self._QUIET:
+            self._owner.last_call = name
+        return getattr(self._lib, name)
 
 
 def parse_rle(text: str) -> np.ndarray:
@@ -312,8 +358,10 @@ class Engine:
 
     def __init__(self, width: int, height: int, ngpus: int = 1, k: int = 1, *, rank: int | None = None,
                  world_size: int = 1, device: int = 0, nccl_id: bytes | None = None,
-                 strips: int | None = None, host_comm: GlooHostComm | None = None):
-        L = load_library()
+                 strips: int | None = None, host_comm: GlooHostComm | None = None,
+                 lib: ctypes.CDLL | None = None):
+        self.last_call = "golhip_create"
+        L = _CallLog(lib if lib is not None else load_library(), self)
         self._L = L
         self._h = ctypes.c_void_p()
         self.host_comm = host_comm  # keeps the ctypes callbacks alive with the handle
@@ -511,10 +559,21 @@ class Engine:
 
     def set_band_rows(self, rows: int):
         self._check(self._L.golhip_set_band_rows(self._h, rows))
+        self.info = self.get_info()
 
     def set_tail_bands(self, bands: int, rows: int):
         self._check(self._L.golhip_set_tail_bands(self._h, bands, rows))
-        self.info = self.get_info()
+
+    def set_graphs(self, mode: int):
+        """Graph replay of step blocks: -1 automatic, 0 never, 1 whenever the plan allows."""
+        self._check(self._L.golhip_set_graphs(self._h, mode))
+
+    def set_count_window(self, generations: int):
+        self._check(self._L.golhip_set_count_window(self._h, generations))
+
+    def set_comm_timeout(self, ms: int):
+        """Deadline of waits on RCCL-dependent work (rank mode): ERR_RCCL when it passes."""
+        self._check(self._L.golhip_set_comm_timeout(self._h, int(ms)))
 
     def launch_kind(self, k: int, counts: bool = False) -> tuple[str, int]:
         """The kernel a k-deep launch runs (with / without per-generation counts): ("stream", 0),

@@ -97,7 +97,12 @@ int golhip_create_strips(int width, int height, int nstrips, int ndevices, int k
  * GOLHIP_NCCL_ID_BYTES produced by golhip_nccl_unique_id() on rank 0 (NULL if world_size == 1).
  * Test hook: with world_size == 1 and the environment variable GOLHIP_RING_SELF=1 the board is a
  * ring of ONE halo'd strip whose halos go through RCCL send/recv to itself (the rank-mode path
- * on a single GPU). */
+ * on a single GPU); GOLHIP_RING_SELF=2 is the same ring with a top-halo receive one row longer
+ * than its send (an exchange that cannot complete: the fail-fast test of golhip_set_comm_timeout).
+ * The communicator is non-blocking: a rank whose peers never join fails after the comm timeout.
+ * GOLHIP_RING_SELF and GOLHIP_STAGE_BYTES (the transfer stage's size in bytes, read at create;
+ * tests shrink it to force many row chunks) are the only environment variables the production
+ * library reads. */
 int golhip_nccl_unique_id(uint8_t *out /* GOLHIP_NCCL_ID_BYTES */);
 int golhip_create_rank(int width, int height, int rank, int world_size, int device, int k,
                        const uint8_t *nccl_id, golhip_t *out);
@@ -227,6 +232,20 @@ int golhip_set_tail_bands(golhip_t h, int bands, int rows);
  * different slab shape when counting. */
 int golhip_launch_kind(golhip_t h, int k, int *kind, int *param);
 int golhip_launch_kind_counts(golhip_t h, int k, int counting, int *kind, int *param);
+/* Captured-graph replay of step blocks on single-strip small boards: -1 automatic (boards whose
+ * launches are short), 0 never, 1 whenever the launch plan allows (tests, tuning). */
+int golhip_set_graphs(golhip_t h, int mode);
+/* Generations of per-turn counts summed per finalize launch (default 4096, minimum 128; tests
+ * shrink it to exercise the flushes).  Synchronises the handle. */
+int golhip_set_count_window(golhip_t h, int generations);
+/* Deadline (ms) of every host wait on work behind an RCCL transfer in rank mode -- the
+ * communicator's set-up at create, a halo exchange, the count all-reduce, a sync -- plus 10x the
+ * modelled time of the stencil work queued since the last sync.  When it passes (or RCCL reports an
+ * asynchronous error) the communicator is aborted and the call returns GOLHIP_ERR_RCCL, with
+ * golhip_last_error naming the rank, the pending operation, its peers, K and its byte count; the
+ * handle then only accepts golhip_destroy.  h == NULL sets the default of later creates (120000).
+ * The reference has no such bound: a dead server stalls Broker.Publish (broker/broker.go:58-84). */
+int golhip_set_comm_timeout(golhip_t h, int64_t ms);
 int golhip_sync(golhip_t h);                         /* wait for all queued device work */
 /* HIP-event timing of golhip_step calls on the handle's first strip (one event pair per call
  * around its back-to-back stencil launches); kernel_time reports the summed span, the number of

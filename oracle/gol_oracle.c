@@ -16,8 +16,9 @@
  *       - broker publish split      broker/broker.go:37-56   (ImageSize/numServers strips)
  *       - Broker.Publish stitch     broker/broker.go:157-180 (ordered concatenation)
  *     It keeps the reference's cost structure (bytes, branches, per-turn row allocation,
- *     servers x threads OS threads per turn, optional full-world copy per server per turn
- *     modelling the gob fan-out of broker/broker.go:51) and is the `cpu_baseline` "port".
+ *     servers x threads workers -- a persistent pool, the goroutine analogue -- and an optional
+ *     full-world copy per server per turn modelling the gob fan-out of broker/broker.go:51) and
+ *     is the `cpu_baseline` "port".
  *
  *  2. oracle_packed_* -- an independent bit-sliced stepper (64 cells per uint64, LSB-first:
  *     bit b of word j is x = 64j+b) used to produce golden vectors at sizes the byte
@@ -86,18 +87,159 @@ static void *ref_calculate_next_state(void *arg) {
     return NULL;
 }
 
+/*
+ * The reference's workers, as a persistent pool (the goroutine analogue): servers x threads
+ * workers are created ONCE per run and handed each turn's work through barriers, so a turn costs
+ * what a Go turn costs -- spawning goroutines is cheap, spawning OS threads per turn is not
+ * (round 3 created 256 pthreads per turn, which dominated the 512^2 figure).  Per turn:
+ *   1. fan-out: the first worker of each server copies the whole world (the server's gob-decoded
+ *      private copy, broker/broker.go:51,64; the servers are separate processes, so the copies run
+ *      concurrently), when fanout_copy != 0;
+ *   2. every worker computes its sub-strip into freshly malloc'd rows (server/server.go:21-31,
+ *      83-97: SplitSize/Threads rows, remainder first);
+ *   3. the calling thread stitches the rows in server then goroutine order (broker/broker.go:168-174,
+ *      server/server.go:98-104) and frees them.
+ */
+typedef struct ref_pool ref_pool;
 typedef struct {
-    size_t bytes;
-    const uint8_t *src;
-    uint8_t *dst;
-} ref_copy_task;
+    ref_pool *pool;
+    int server, index;
+} ref_worker;
 
-/* one server's gob-decoded private copy of the whole world: the servers are separate processes
- * (broker/broker.go:58-66 calls them from one goroutine each), so their copies run concurrently */
-static void *ref_copy_world(void *arg) {
-    ref_copy_task *c = (ref_copy_task *)arg;
-    memcpy(c->dst, c->src, c->bytes);
+struct ref_pool {
+    int n, servers, threads, fanout;
+    int nw;                       /* servers * threads */
+    const uint8_t *world;         /* this turn's input */
+    uint8_t **rows;               /* Request.World as [][]byte: row slices into `world` */
+    uint8_t **server_block;       /* fan-out copies, n*n bytes per server */
+    uint8_t ***server_world;      /* row slices into them */
+    ref_task *tasks;              /* nw sub-strips (fixed split) */
+    ref_worker *workers;
+    pthread_t *tids;
+    pthread_barrier_t start, copied, done;
+    int quit;
+};
+
+static void *ref_worker_main(void *arg) {
+    ref_worker *w = (ref_worker *)arg;
+    ref_pool *p = w->pool;
+    for (;;) {
+        pthread_barrier_wait(&p->start);
+        if (p->quit) break;
+        if (p->fanout && w->index == 0)
+            memcpy(p->server_block[w->server], p->world, (size_t)p->n * p->n);
+        pthread_barrier_wait(&p->copied);
+        ref_calculate_next_state(&p->tasks[w->server * p->threads + w->index]);
+        pthread_barrier_wait(&p->done);
+    }
     return NULL;
+}
+
+static void ref_pool_destroy(ref_pool *p) {
+    if (!p) return;
+    if (p->tids) {
+        p->quit = 1;
+        pthread_barrier_wait(&p->start);
+        for (int i = 0; i < p->nw; i++) pthread_join(p->tids[i], NULL);
+        pthread_barrier_destroy(&p->start);
+        pthread_barrier_destroy(&p->copied);
+        pthread_barrier_destroy(&p->done);
+    }
+    for (int s = 0; p->server_block && s < p->servers; s++) {
+        free(p->server_world[s]);
+        free(p->server_block[s]);
+    }
+    for (int i = 0; p->tasks && i < p->nw; i++) free(p->tasks[i].rows_out);
+    free(p->server_world);
+    free(p->server_block);
+    free(p->tasks);
+    free(p->workers);
+    free(p->tids);
+    free(p->rows);
+    free(p);
+}
+
+/* n % servers != 0 is rejected: the reference's own index arithmetic drops rows there
+ * (SURVEY.md section 0 fact 5). */
+static ref_pool *ref_pool_create(int n, int threads, int servers, int fanout_copy) {
+    if (n <= 0 || threads <= 0 || servers <= 0 || n % servers != 0) return NULL;
+    ref_pool *p = (ref_pool *)calloc(1, sizeof(ref_pool));
+    p->n = n;
+    p->servers = servers;
+    p->threads = threads;
+    p->fanout = fanout_copy;
+    p->nw = servers * threads;
+    p->rows = (uint8_t **)malloc(sizeof(uint8_t *) * (size_t)n);
+    p->tasks = (ref_task *)calloc((size_t)p->nw, sizeof(ref_task));
+    p->workers = (ref_worker *)calloc((size_t)p->nw, sizeof(ref_worker));
+    p->server_block = (uint8_t **)calloc((size_t)servers, sizeof(uint8_t *));
+    p->server_world = (uint8_t ***)calloc((size_t)servers, sizeof(uint8_t **));
+    if (fanout_copy)
+        for (int s = 0; s < servers; s++) {
+            p->server_block[s] = (uint8_t *)malloc((size_t)n * n);
+            p->server_world[s] = (uint8_t **)malloc(sizeof(uint8_t *) * (size_t)n);
+            if (!p->server_block[s] || !p->server_world[s]) {
+                ref_pool_destroy(p);
+                return NULL;
+            }
+            for (int y = 0; y < n; y++) p->server_world[s][y] = p->server_block[s] + (size_t)y * n;
+        }
+    /* broker publish: splitSize := ImageSize / numServers (broker/broker.go:38-51);
+     * GolOP.Work: splitSize := req.SplitSize / req.Threads (server/server.go:83-97) */
+    int split = n / servers, diff = n % servers, pos = 0;
+    for (int s = 0; s < servers; s++) {
+        int start = pos;
+        pos += split - 1;
+        if (diff != 0) { pos++; diff--; }
+        pos++;
+        int tsplit = split / threads, tdiff = split % threads, tpos = start;
+        for (int i = 0; i < threads; i++) {
+            int tstart = tpos;
+            tpos += tsplit - 1;
+            if (tdiff > 0) { tpos++; tdiff--; }
+            int tend = tpos;
+            tpos++;
+            ref_task *t = &p->tasks[s * threads + i];
+            t->image_size = n;
+            t->start = tstart;
+            t->end = tend;
+            t->world = fanout_copy ? p->server_world[s] : p->rows;
+            int h = tend - tstart + 1;
+            t->rows_out = (uint8_t **)malloc(sizeof(uint8_t *) * (size_t)(h > 0 ? h : 1));
+        }
+    }
+    pthread_barrier_init(&p->start, NULL, (unsigned)p->nw + 1);
+    pthread_barrier_init(&p->copied, NULL, (unsigned)p->nw);
+    pthread_barrier_init(&p->done, NULL, (unsigned)p->nw + 1);
+    p->tids = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)p->nw);
+    for (int s = 0; s < servers; s++)
+        for (int i = 0; i < threads; i++) {
+            ref_worker *w = &p->workers[s * threads + i];
+            w->pool = p;
+            w->server = s;
+            w->index = i;
+            pthread_create(&p->tids[s * threads + i], NULL, ref_worker_main, w);
+        }
+    return p;
+}
+
+/* One turn through the pool: world -> out (n*n bytes each).  Returns the rows produced. */
+static int ref_pool_step(ref_pool *p, const uint8_t *world, uint8_t *out) {
+    const int n = p->n;
+    p->world = world;
+    for (int y = 0; y < n; y++) p->rows[y] = (uint8_t *)world + (size_t)y * n;
+    pthread_barrier_wait(&p->start);
+    pthread_barrier_wait(&p->done);
+    int produced = 0;
+    for (int i = 0; i < p->nw; i++) {
+        int h = p->tasks[i].end - p->tasks[i].start + 1;
+        for (int y = 0; y < h; y++) {
+            if (produced < n) memcpy(out + (size_t)produced * n, p->tasks[i].rows_out[y], (size_t)n);
+            produced++;
+            free(p->tasks[i].rows_out[y]);
+        }
+    }
+    return produced;
 }
 
 /*
@@ -113,97 +255,24 @@ static void *ref_copy_world(void *arg) {
  */
 int oracle_ref_step(int n, const uint8_t *world, uint8_t *out, int threads, int servers,
                     int fanout_copy) {
-    if (n <= 0 || threads <= 0 || servers <= 0) return -1;
-    if (n % servers != 0) return -1;
-    /* Request.World as [][]byte (row slices into the caller's buffer) */
-    uint8_t **rows = (uint8_t **)malloc(sizeof(uint8_t *) * (size_t)n);
-    for (int y = 0; y < n; y++) rows[y] = (uint8_t *)world + (size_t)y * n;
-
-    int ntask_max = servers * threads;
-    ref_task *tasks = (ref_task *)calloc((size_t)ntask_max, sizeof(ref_task));
-    pthread_t *tids = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)ntask_max);
-    uint8_t ***server_world = (uint8_t ***)calloc((size_t)servers, sizeof(uint8_t **));
-    uint8_t **server_block = (uint8_t **)calloc((size_t)servers, sizeof(uint8_t *));
-
-    if (fanout_copy) {
-        pthread_t *ctids = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)servers);
-        ref_copy_task *ct = (ref_copy_task *)malloc(sizeof(ref_copy_task) * (size_t)servers);
-        for (int s = 0; s < servers; s++) {
-            server_block[s] = (uint8_t *)malloc((size_t)n * n);
-            ct[s].bytes = (size_t)n * n;
-            ct[s].src = world;
-            ct[s].dst = server_block[s];
-            pthread_create(&ctids[s], NULL, ref_copy_world, &ct[s]);
-        }
-        for (int s = 0; s < servers; s++) pthread_join(ctids[s], NULL);
-        free(ctids);
-        free(ct);
-    }
-    /* broker publish: splitSize := ImageSize / numServers (broker/broker.go:38-51) */
-    int split = n / servers, diff = n % servers, pos = 0, nt = 0;
-    for (int s = 0; s < servers; s++) {
-        int start = pos;
-        pos += split - 1;
-        if (diff != 0) { pos++; diff--; }
-        pos++;
-        uint8_t **w = rows;
-        if (fanout_copy) { /* the server's private copy of the whole world (made above) */
-            server_world[s] = (uint8_t **)malloc(sizeof(uint8_t *) * (size_t)n);
-            for (int y = 0; y < n; y++) server_world[s][y] = server_block[s] + (size_t)y * n;
-            w = server_world[s];
-        }
-        /* GolOP.Work: splitSize := req.SplitSize / req.Threads (server/server.go:83-97),
-         * req.SplitSize is n/servers, req.StartY is this strip's start. */
-        int tsplit = split / threads, tdiff = split % threads, tpos = start;
-        for (int i = 0; i < threads; i++) {
-            int tstart = tpos;
-            tpos += tsplit - 1;
-            if (tdiff > 0) { tpos++; tdiff--; }
-            int tend = tpos;
-            tpos++;
-            ref_task *t = &tasks[nt];
-            t->image_size = n;
-            t->start = tstart;
-            t->end = tend;
-            t->world = w;
-            int h = tend - tstart + 1;
-            t->rows_out = (uint8_t **)malloc(sizeof(uint8_t *) * (size_t)(h > 0 ? h : 1));
-            pthread_create(&tids[nt], NULL, ref_calculate_next_state, t);
-            nt++;
-        }
-    }
-    /* stitch in server order then goroutine order */
-    int produced = 0;
-    for (int i = 0; i < nt; i++) {
-        pthread_join(tids[i], NULL);
-        int h = tasks[i].end - tasks[i].start + 1;
-        for (int y = 0; y < h; y++) {
-            if (produced < n) memcpy(out + (size_t)produced * n, tasks[i].rows_out[y], (size_t)n);
-            produced++;
-            free(tasks[i].rows_out[y]);
-        }
-        free(tasks[i].rows_out);
-    }
-    for (int s = 0; s < servers; s++) {
-        free(server_world[s]);
-        free(server_block[s]);
-    }
-    free(server_world);
-    free(server_block);
-    free(tids);
-    free(tasks);
-    free(rows);
+    ref_pool *p = ref_pool_create(n, threads, servers, fanout_copy);
+    if (!p) return -1;
+    int produced = ref_pool_step(p, world, out);
+    ref_pool_destroy(p);
     return produced;
 }
 
-/* Run `turns` reference turns in place (world n*n bytes).  counts (nullable, len turns)
- * receives the alive count after each completed turn, as gol/distributor.go:153-166,186. */
+/* Run `turns` reference turns in place (world n*n bytes) on one worker pool.  counts (nullable,
+ * len turns) receives the alive count after each completed turn, as gol/distributor.go:153-166,186
+ * (the controller's scan, one thread). */
 int oracle_ref_run(int n, uint8_t *world, long turns, int threads, int servers, int fanout_copy,
                    int64_t *counts) {
+    ref_pool *p = ref_pool_create(n, threads, servers, fanout_copy);
+    if (!p) return -1;
     uint8_t *tmp = (uint8_t *)malloc((size_t)n * n);
     for (long t = 0; t < turns; t++) {
-        int r = oracle_ref_step(n, world, tmp, threads, servers, fanout_copy);
-        if (r != n) { free(tmp); return -1; }
+        int r = ref_pool_step(p, world, tmp);
+        if (r != n) { free(tmp); ref_pool_destroy(p); return -1; }
         memcpy(world, tmp, (size_t)n * n);
         if (counts) {
             int64_t c = 0;
@@ -212,6 +281,7 @@ int oracle_ref_run(int n, uint8_t *world, long turns, int threads, int servers, 
         }
     }
     free(tmp);
+    ref_pool_destroy(p);
     return 0;
 }
 

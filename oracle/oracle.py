@@ -187,6 +187,22 @@ def digest_words(words: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(words, dtype="<u8").tobytes()).hexdigest()
 
 
+# Board digest that row strips can compute apart ("checksum of checksums"): SHA-256 of the
+# concatenated SHA-256s of consecutive DIGEST_CHUNK_ROWS-row chunks of the packed little-endian
+# uint64 rows.  A rank whose strip starts on a chunk boundary hashes its own chunks; rank 0 hashes
+# the gathered list (bench.py's parity.digest).  4096 divides every strip height the benches use.
+DIGEST_CHUNK_ROWS = 4096
+
+
+def chunk_digests(words: np.ndarray, chunk_rows: int = DIGEST_CHUNK_ROWS) -> list[bytes]:
+    w = np.ascontiguousarray(words, dtype="<u8")
+    return [hashlib.sha256(w[y:y + chunk_rows].tobytes()).digest() for y in range(0, w.shape[0], chunk_rows)]
+
+
+def board_digest(chunks: list[bytes]) -> str:
+    return hashlib.sha256(b"".join(chunks)).hexdigest()
+
+
 def read_alive_csv(path) -> dict[int, int]:
     """check/alive/*.csv: header completed_turns,alive_cells (count_test.go:78-89)."""
     out = {}

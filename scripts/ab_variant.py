@@ -13,6 +13,8 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "distributed-gol_amd"))
+# the tuning build holds the selectable variants / forced shapes (lib/ has only production)
+os.environ.setdefault("GOLHIP_LIB", str(ROOT / "distributed-gol_amd" / "lib_tuning" / "libgolhip.so"))
 import torch  # noqa: E402,F401
 import golhip  # noqa: E402
 

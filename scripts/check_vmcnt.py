@@ -128,6 +128,9 @@ def vmcnt(ins: str) -> int | None:
     return int(m.group(1)) if m else None
 
 
+LINEARIZE_NOTES: list[str] = []
+
+
 def linearize(code, hand: set[int]) -> list[int]:
     """Program order with the innermost loop that holds a hand wait unrolled twice (the steady
     loop: its first iteration is entered from the unrolled fill, the second from its own
@@ -135,12 +138,20 @@ def linearize(code, hand: set[int]) -> list[int]:
     index = {a: i for i, (a, _, _) in enumerate(code)}
     best = None
     for i, (a, ins, t) in enumerate(code):
-        # s_cbranch_execz skips a lane-masked region when no lane is active; the ring code's masked
-        # regions (PRE's lane-0 65th-word DMA) always have one, so the branch is never taken -- the
-        # compiler may still close the steady loop with it (rotated loop), which must not be read
-        # as the loop's back edge
+        # s_cbranch_execz skips a lane-masked region when no lane is active.  A BACKWARD execz is
+        # skipped only when the fall-through path reaches the same target too (a later branch back
+        # to it closes the loop, so the execz is an early exit of a region inside it, never the
+        # steady loop's own back edge); otherwise it is kept as a back-edge candidate and reported
+        # (LINEARIZE_NOTES), so the guard cannot silently pick a different loop.  The ring code
+        # itself has no masked regions since PRE's 65th word became a whole-wave DMA; the
+        # prodmask variant's `if (live)` around the whole ring is a FORWARD execz.
         if ins.startswith("s_cbranch_execz"):
-            continue
+            if t is None or t >= a:
+                continue
+            if any(t2 == t for _, _, t2 in code[i + 1:]):
+                continue
+            LINEARIZE_NOTES.append(f"backward s_cbranch_execz at {a:#x} -> {t:#x} with no later "
+                                   "back edge to its target: kept as a loop back edge")
         if t is not None and t < a and t in index:
             lo = index[t]
             if any(lo <= h <= i for h in hand) and (best is None or i - lo < best[1] - best[0]):
@@ -260,6 +271,8 @@ def main() -> int:
         print(f"FAIL {obj} {name}")
         for e in errs:
             print(f"     {e}")
+    for n in sorted(set(LINEARIZE_NOTES)):
+        print(f"warn: {n}")
     print(f"check_vmcnt: {checked} LDS-DMA kernels checked, {len(failures)} failed")
     if expect_fail:
         if failures:

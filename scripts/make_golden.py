@@ -114,6 +114,40 @@ def weak_small():
     return out
 
 
+def digests():
+    """Whole-board digests of the bench boards (bench.py parity.digest_ok): the 65536 x 65536*N
+    board, random p=0.5 seed 3, for N = 1 (configs[2]) and the weak-scaling N = 2, 4, 8, after
+    25 turns (the driver's --warmup 5 --steps 20) and 1008 (the default --warmup 8 --steps 1000).
+    oracle.board_digest of 4096-row chunk digests, so each rank hashes its own strip."""
+    out = {}
+    for n in (1, 2, 4, 8):
+        w = oracle.init_random(65536, 65536 * n, seed=3)
+        t = time.time()
+        oracle.packed_run_words(w, 25, threads=8)
+        d25 = oracle.board_digest(oracle.chunk_digests(w))
+        oracle.packed_run_words(w, 1008 - 25, threads=8)
+        d1008 = oracle.board_digest(oracle.chunk_digests(w))
+        out[f"digest_65536x{65536 * n}"] = {
+            "width": 65536, "height": 65536 * n, "seed": 3, "chunk_rows": oracle.DIGEST_CHUNK_ROWS,
+            "board_digest": {"25": d25, "1008": d1008}, "oracle_seconds": round(time.time() - t, 1)}
+        del w
+        print("digests", n, out[f"digest_65536x{65536 * n}"]["oracle_seconds"], "s", flush=True)
+    return out
+
+
+def digests_small():
+    """Board digests of the small weak-scaling boards the rank-path tests run bench.main() on
+    (4096 x 4096*N and 8192 x 8192*N, N = 2, 3, seed 3) after 25 turns (--warmup 5 --steps 20)."""
+    out = {}
+    for w, n in ((4096, 2), (4096, 3), (8192, 2), (8192, 3)):
+        b = oracle.init_random(w, w * n, seed=3)
+        oracle.packed_run_words(b, 25, threads=8)
+        out[f"digest_{w}x{w * n}"] = {"width": w, "height": w * n, "seed": 3,
+                                      "chunk_rows": oracle.DIGEST_CHUNK_ROWS,
+                                      "board_digest": {"25": oracle.board_digest(oracle.chunk_digests(b))}}
+    return out
+
+
 def cfg5_board():
     import golhip
 

@@ -8,10 +8,9 @@ K=${1:-8}; shift || true
 OUT=gpurun_out/pmc_k${K}
 mkdir -p $OUT
 export TMPDIR=/tmp
-# GOLHIP_FIXED_K: the launches are exactly K deep (the planner would run its best depth <= K: at
+# --fixed-k: the launches are exactly K deep (the planner would run its best depth <= K: at
 # 65536^2 that is 12 for K = 16, which the round-3 "pmc_k16" passes caught instead)
-export GOLHIP_FIXED_K=1
-BENCH="python3 bench.py --no-cpu --no-sweep --no-strong --no-flips --no-configs --preheat-ms 0 --steps $((2*K)) --warmup 0 --k $K $*"
+BENCH="python3 bench.py --no-cpu --no-sweep --no-strong --no-flips --no-configs --preheat-ms 0 --fixed-k --steps $((2*K)) --warmup 0 --k $K $*"
 i=0
 for CTRS in "FETCH_SIZE" "WRITE_SIZE" \
             "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU" \

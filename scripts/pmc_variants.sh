@@ -5,6 +5,8 @@ K=${1:-8}; VARS=${2:-"chainlds chainlds2"}; SIZE=${3:-65536}
 OUT=gpurun_out/pmcv_k${K}
 mkdir -p $OUT
 export TMPDIR=/tmp
+# the variants live in the tuning build (lib/libgolhip.so has only the production kernels)
+export GOLHIP_LIB=$PWD/distributed-gol_amd/lib_tuning/libgolhip.so
 for V in $VARS; do
   export GOLHIP_VARIANT=$V
   BENCH="python3 bench.py --no-cpu --no-sweep --steps $((4*K)) --warmup $K --k $K --size $SIZE"

@@ -14,6 +14,8 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "distributed-gol_amd"))
+# the tuning build holds the selectable variants / forced shapes (lib/ has only production)
+os.environ.setdefault("GOLHIP_LIB", str(ROOT / "distributed-gol_amd" / "lib_tuning" / "libgolhip.so"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402,F401
 

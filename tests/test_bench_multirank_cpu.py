@@ -34,8 +34,8 @@ def _free_port():
 
 
 class _Info:
-    def __init__(self, rows):
-        self.rows = rows
+    def __init__(self, rows, y0, width):
+        self.rows, self.y0, self.width = rows, y0, width
 
 
 class FakeEngine:
@@ -54,7 +54,8 @@ class FakeEngine:
         self.width, self.height, self.rows, self.k = width, height, rows, k
         self.rank, self.world = rank, world_size
         self.buf = np.zeros((rows + 2 * k, width // 64), dtype=np.uint64)
-        self.info = _Info(rows)
+        self.info = _Info(rows, self.y0, width)
+        self.last_call = "golhip_create_rank"
         self.turn = 0
         self.timed = False
         self.t_ms = 0.0
@@ -73,6 +74,13 @@ class FakeEngine:
 
     def set_band_rows(self, n):
         pass
+
+    def set_fixed_k(self, fixed):
+        pass
+
+    def store_words(self):
+        FakeEngine.log.append(("store_words",))
+        return self.buf[self.k:self.k + self.rows].copy()
 
     def _block(self, K):
         import golhip
@@ -203,7 +211,9 @@ def test_bench_rank_path_cpu(tmp_path, world):
     assert line["cold_start"]["preheat_turns"] >= 16
     assert line["strong_262144"]["rows_per_gpu"] == -(-2048 // world)
     # the weak-scaling board (4096 x 4096*N, seed 3) is pinned: parity against the oracle golden
-    # at turn warmup + steps, in both the pre-heated and the cold-start pass
+    # at turn warmup + steps, in both the pre-heated and the cold-start pass; and bit for bit:
+    # every rank hashed its strip, rank 0 the gathered chunk digests == the oracle's board digest
     assert line["parity"] is not None and line["parity"]["turn"] == 25
     assert line["parity"]["ok"] and line["parity"]["cold_start_ok"], line["parity"]
+    assert line["parity"]["digest_ok"] is True, line["parity"]
     assert line["untimed_generations_before_value"] == 5 + 25 + line["cold_start"]["preheat_turns"]

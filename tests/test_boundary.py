@@ -40,6 +40,32 @@ def test_library_is_gfx950_code(golhip):
     assert b"gfx950" in data
 
 
+# the tuning build's selectors (golhip_internal.hpp): the production library must not even hold
+# their names, so a stray environment variable cannot change its kernels
+TUNING_SELECTORS = ["GOLHIP_VARIANT", "GOLHIP_SPLIT", "GOLHIP_TILE", "GOLHIP_SLAB", "GOLHIP_BAND_ROWS",
+                    "GOLHIP_FIXED_K", "GOLHIP_LDS_PAD", "GOLHIP_STEP1", "GOLHIP_GRAPHS",
+                    "GOLHIP_COUNT_WINDOW"]
+
+
+def test_production_library_reads_only_documented_hooks():
+    """lib/libgolhip.so holds no tuning selector (the `strings | grep GOLHIP_VARIANT` check) and only
+    the two documented test hooks; lib_tuning/libgolhip.so holds the selectors."""
+    prod = (PKG / "lib" / "libgolhip.so").read_bytes()
+    names = set(re.findall(rb"GOLHIP_[A-Z][A-Z0-9_]+", prod))
+    assert names == {b"GOLHIP_RING_SELF", b"GOLHIP_STAGE_BYTES"}, names
+    tuning = (PKG / "lib_tuning" / "libgolhip.so").read_bytes()
+    for sel in TUNING_SELECTORS:
+        assert sel.encode() in tuning, sel
+    # the experiment harness stays out of the shipped library: it is several times smaller
+    assert len(prod) * 3 < len(tuning), (len(prod), len(tuning))
+
+
+def test_tuning_library_exports_the_same_abi(golhip):
+    out = subprocess.check_output(["nm", "-D", "--defined-only", str(PKG / "lib_tuning" / "libgolhip.so")],
+                                  text=True)
+    assert set(re.findall(r" T (golhip_\w+)", out)) >= set(header_functions())
+
+
 def test_version_and_strerror(golhip):
     lib = golhip.load_library()
     assert lib.golhip_version() >= 100

@@ -1,0 +1,118 @@
+"""RCCL fail-fast on one GPU: a rank-mode engine whose RCCL work cannot complete returns
+GOLHIP_ERR_RCCL within its deadline (golhip_set_comm_timeout), naming the pending transfer,
+instead of hanging the run (the reference has no such bound: a dead server stalls
+Broker.Publish forever, broker/broker.go:58-84).
+
+Each case runs in a FRESH process under its own time limit, so a failure of the deadline itself
+ends in a killed child, not a hung test session:
+  * exchange: the ring-of-one hook GOLHIP_RING_SELF=2 posts a top-halo receive one row longer than
+    the matching send -- the K-row exchange can never complete as posted;
+  * init: rank 0 of a 2-rank communicator whose rank 1 never joins -- ncclCommInitRankConfig
+    (non-blocking) never finishes its set-up.
+"""
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+from conftest import PKG
+
+pytestmark = pytest.mark.gpu
+
+CHILD = r"""
+import json, sys, time
+sys.path.insert(0, sys.argv[1])
+import torch  # one HIP runtime per process (golhip.py)
+import golhip
+case, timeout_ms = sys.argv[2], int(sys.argv[3])
+golhip.set_default_comm_timeout(timeout_ms)
+out = {"case": case}
+t0 = time.perf_counter()
+try:
+    if case == "exchange":
+        e = golhip.Engine(640, 64, k=4, rank=0, world_size=1, device=0)
+        out["halo_rows"] = e.info.halo_rows
+        e.init_random(5)
+        t0 = time.perf_counter()
+        e.step(9)
+        e.sync()
+        out["completed"] = True
+    else:
+        golhip.Engine(640, 64, k=4, rank=0, world_size=2, device=0, nccl_id=golhip.nccl_unique_id())
+        out["completed"] = True
+except golhip.GolHipError as err:
+    out["code"] = err.code
+    out["msg"] = str(err)
+out["seconds"] = time.perf_counter() - t0
+t1 = time.perf_counter()
+if case == "exchange" and "code" in out:
+    # the handle refuses further device work with the same error, and destroys without hanging
+    try:
+        e.step(1)
+        e.sync()
+        out["after"] = "ok"
+    except golhip.GolHipError as err:
+        out["after"] = err.code
+    e.close()
+out["teardown_seconds"] = time.perf_counter() - t1
+print(json.dumps(out), flush=True)
+"""
+
+
+def run_child(case, timeout_ms, ring_self=None):
+    env = dict(os.environ)
+    env.pop("GOLHIP_RING_SELF", None)
+    if ring_self:
+        env["GOLHIP_RING_SELF"] = ring_self
+    p = subprocess.run(["timeout", "-k", "10", "150", sys.executable, "-c", CHILD, str(PKG), case,
+                        str(timeout_ms)], env=env, capture_output=True, text=True, timeout=200)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert p.returncode == 0 and lines, (p.returncode, p.stdout[-2000:], p.stderr[-2000:])
+    return json.loads(lines[-1])
+
+
+def test_exchange_that_cannot_complete_fails_fast(golhip):
+    timeout_ms = 3000
+    t = time.perf_counter()
+    out = run_child("exchange", timeout_ms, ring_self="2")
+    assert out.get("halo_rows") == 4
+    assert not out.get("completed"), out
+    assert out["code"] == golhip.ERR_RCCL, out
+    # within the deadline (+ the modelled time of the queued work and a margin), not at a hang
+    assert out["seconds"] < timeout_ms / 1e3 + 20, out
+    msg = out["msg"]
+    # golhip_last_error names the rank, the pending operation, its peers, K and the byte count
+    assert "rank 0 of 1" in msg and "K = 4" in msg and "bytes" in msg and "aborted" in msg, msg
+    assert "<- rank 0" in msg and "-> rank 0" in msg, msg
+    assert out["after"] == golhip.ERR_RCCL, out
+    assert out["teardown_seconds"] < timeout_ms / 1e3 + 20, out
+    assert time.perf_counter() - t < 150
+
+
+def test_peer_that_never_joins_fails_fast_at_create(golhip):
+    timeout_ms = 3000
+    out = run_child("init", timeout_ms)
+    assert not out.get("completed"), out
+    assert out["code"] == golhip.ERR_RCCL, out
+    assert out["seconds"] < timeout_ms / 1e3 + 30, out
+    assert "rank 0 of 2" in out["msg"] and "ncclCommInitRankConfig" in out["msg"], out["msg"]
+
+
+def test_ring_of_one_still_exchanges_with_a_deadline(golhip, oracle, monkeypatch):
+    """The non-blocking communicator and the polled waits leave the working path bit-exact: the
+    ring of one under a short deadline, every count and the board equal to the oracle."""
+    monkeypatch.setenv("GOLHIP_RING_SELF", "1")
+    w, h, k = 640, 77, 8
+    words = oracle.init_random(w, h, seed=77)
+    with golhip.Engine(w, h, k=k, rank=0, world_size=1, device=0) as e:
+        e.set_comm_timeout(5000)
+        e.load_words(words)
+        counts = e.step(3 * k + 5, counts=True)
+        got = e.store_words()
+    ref = words.copy()
+    ref_counts = oracle.packed_run_words(ref, 3 * k + 5)
+    assert (got == ref).all()
+    assert (counts.astype("int64") == ref_counts).all()

@@ -13,9 +13,9 @@ SIZES = [16, 64, 512]
 KS = [1, 2, 4, 8, 16, 32]
 
 
-def run_engine(golhip, board, turns, k=1, counts=False, band_rows=0):
+def run_engine(golhip, board, turns, k=1, counts=False, band_rows=0, lib=None):
     h, w = board.shape
-    with golhip.Engine(w, h, k=k) as e:
+    with golhip.Engine(w, h, k=k, lib=lib) as e:
         e.set_fixed_k(True)  # launches exactly k deep (the planner would pick its fastest <= k)
         if band_rows:
             e.set_band_rows(band_rows)
@@ -90,18 +90,14 @@ def test_flips_match_oracle(golhip, oracle):
             assert [tuple(c) for c in e.flips().tolist()] == oracle.flips(gen_prev, after), n
 
 
-@pytest.mark.parametrize("variant", ["prod", "driftlds", "drift62", "pre63", "prodmask"])
-@pytest.mark.parametrize("k", [1, 2, 6, 12, 16, 32])
-@pytest.mark.parametrize("strips", [1, 3])
-def test_tracked_flips_every_depth(golhip, oracle, monkeypatch, variant, k, strips):
-    """Flips tracking at every launch depth, both drift geometries and the multi-strip (halo)
-    path: golhip_flips after a k-deep step == the oracle's diff of the last two generations."""
-    monkeypatch.setenv("GOLHIP_VARIANT", variant)
+def tracked_flips_every_depth(golhip, oracle, k, strips, lib=None):
+    """Flips tracking at a launch depth on the single-strip and multi-strip (halo) paths:
+    golhip_flips after a k-deep step == the oracle's diff of the last two generations."""
     h, w = 111, 4160
     if h // strips < k:
         pytest.skip("strip shorter than k")
     words = oracle.init_random(w, h, seed=k * 10 + strips)
-    with golhip.Engine(w, h, ngpus=1, k=k, strips=strips) as e:
+    with golhip.Engine(w, h, ngpus=1, k=k, strips=strips, lib=lib) as e:
         e.set_fixed_k(True)
         e.track_flips(True)
         e.load_words(words)
@@ -113,14 +109,21 @@ def test_tracked_flips_every_depth(golhip, oracle, monkeypatch, variant, k, stri
             assert [tuple(c) for c in e.flips().tolist()] == oracle.flips(gen_prev, after), n
 
 
-def test_tracked_flips_small_board_graphs(golhip, oracle, monkeypatch):
+@pytest.mark.parametrize("k", [1, 2, 6, 12, 16, 32])
+@pytest.mark.parametrize("strips", [1, 3])
+def test_tracked_flips_every_depth(golhip, oracle, k, strips):
+    """The production kernels (the other drift geometries: tests/test_gpu_tuning.py)."""
+    tracked_flips_every_depth(golhip, oracle, k, strips)
+
+
+def test_tracked_flips_small_board_graphs(golhip, oracle):
     """Small boards replay captured graphs; with tracking the last launch stays a plain,
     flips-writing launch."""
-    monkeypatch.setenv("GOLHIP_GRAPHS", "1")
     _, _, board = oracle.read_pgm(REF / "images/512x512.pgm")
     gen_prev, _ = oracle.packed_run(board, 299)
     expected, _ = oracle.packed_run(board, 300)
     with golhip.Engine(512, 512, k=16) as e:
+        e.set_graphs(1)
         e.track_flips(True)
         e.load(board)
         e.step(300)
@@ -357,14 +360,14 @@ def test_row_strips_bytes_roundtrip(golhip, oracle):
 
 
 @pytest.mark.parametrize("k", [1, 8, 32])
-def test_graph_replay_matches_launches(golhip, oracle, monkeypatch, k):
+def test_graph_replay_matches_launches(golhip, oracle, k):
     """Small boards replay captured graphs of step blocks; both buffer parities, with and
     without per-turn counts, must equal the oracle."""
     w, h = 1000, 300
     words = oracle.init_random(1024, h, seed=k)[:, :]
     board = oracle.unpack(words, w)
-    monkeypatch.setenv("GOLHIP_GRAPHS", "1")
     with golhip.Engine(w, h, k=k) as e:
+        e.set_graphs(1)
         e.load(board)
         e.step(1)                                  # odd parity before the graphs
         c1 = e.step(300, counts=True)              # graph replays + tail blocks
@@ -375,46 +378,6 @@ def test_graph_replay_matches_launches(golhip, oracle, monkeypatch, k):
     assert np.array_equal(got, exp)
     assert np.array_equal(c1.astype(np.int64), exp_counts[1:301])
     assert len(cells) == int((exp == 255).sum())
-
-
-@pytest.mark.parametrize("variant", ["chainlds", "driftlds", "driftzip", "drift62", "driftnf", "pre63", "skewlds", "chainlds2",
-                                     "skewlds2", "chain", "skew", "chain2", "skew2"])
-@pytest.mark.parametrize("k", [1, 6, 16])
-def test_every_kernel_variant(golhip, oracle, monkeypatch, variant, k):
-    """Every stencil variant (chained/skewed levels, 1 or 2 words per lane, register or LDS-DMA
-    prefetch) on the shapes that stress wrap, halo lanes and band seams."""
-    monkeypatch.setenv("GOLHIP_VARIANT", variant)
-    for (h, w) in [(77, 640), (16, 16), (300, 4160)]:
-        rng = np.random.default_rng(h + w + k)
-        board = ((rng.random((h, w)) < 0.4) * 255).astype(np.uint8)
-        turns = 2 * k + 1
-        exp, exp_counts = oracle.packed_run(board, turns)
-        for band in (0, 7):
-            out, counts, _, _ = run_engine(golhip, board, turns, k=k, counts=True, band_rows=band)
-            assert np.array_equal(out, exp), (variant, k, h, w, band)
-            assert np.array_equal(counts.astype(np.int64), exp_counts), (variant, k, h, w, band)
-
-
-@pytest.mark.parametrize("variant", ["driftlds", "driftzip", "drift62", "pre63", "prodmask"])
-@pytest.mark.parametrize("k", [2, 4, 6, 8, 10, 12, 14, 16, 32])
-def test_drift_variant_every_k(golhip, oracle, monkeypatch, variant, k):
-    """The drifting-sum stencils (rows move one bit east per level, one DPP per level update) --
-    half-word-halo chunks (driftlds), 62-word chunks (drift62), 62-word chunks with two steps
-    interleaved (driftzip) and 63-word chunks of rows pre-shifted K bits west (pre63, its 65th-word
-    DMA and no store realignment): every launch depth, per-turn counts (drifted count windows), multi-
-    chunk rows with a partial last chunk and widths that are not a multiple of 128 (replicated
-    torus)."""
-    monkeypatch.setenv("GOLHIP_VARIANT", variant)
-    for (h, w) in [(64, 4160), (35, 2016), (130, 8192), (9, 96), (20, 1984), (24, 3968)]:
-        rng = np.random.default_rng(h * 31 + w + k)
-        board = ((rng.random((h, w)) < 0.37) * 255).astype(np.uint8)
-        turns = 3 * k + 5
-        exp, exp_counts = oracle.packed_run(board, turns)
-        for band in (0, 3, 40):
-            out, counts, cells, count = run_engine(golhip, board, turns, k=k, counts=True, band_rows=band)
-            assert np.array_equal(out, exp), (k, h, w, band)
-            assert np.array_equal(counts.astype(np.int64), exp_counts), (k, h, w, band)
-            assert count == int((exp == 255).sum())
 
 
 @pytest.mark.parametrize("k", [2, 8, 12, 14, 16])
@@ -460,26 +423,8 @@ def test_graded_tail_bands(golhip, oracle, k):
                 assert np.array_equal(c.astype(np.int64), exp_counts), (k, h, w, band, tail)
 
 
-@pytest.mark.parametrize("split,k", [(s, k) for k in (4, 6, 8, 16, 32) for s in (2, 4, 8)
-                                     if k % s == 0])  # levels split evenly over the waves
-def test_level_split_kernel(golhip, oracle, monkeypatch, split, k):
-    """The level-split stencil (gol_stencil_split: the K levels of a band over S waves of one
-    workgroup, rows handed off through LDS, lockstep barriers) on the shapes that stress wrap,
-    half-word halos, short last bands and band seams, with per-turn counts."""
-    monkeypatch.setenv("GOLHIP_SPLIT", str(split))
-    for (h, w) in [(77, 640), (16, 16), (300, 4160), (129, 200)]:
-        rng = np.random.default_rng(h * 7 + w + k + split)
-        board = ((rng.random((h, w)) < 0.4) * 255).astype(np.uint8)
-        turns = 3 * k + 1
-        exp, exp_counts = oracle.packed_run(board, turns)
-        for band in (0, 5):
-            out, counts, _, _ = run_engine(golhip, board, turns, k=k, counts=True, band_rows=band)
-            assert np.array_equal(out, exp), (split, k, h, w, band)
-            assert np.array_equal(counts.astype(np.int64), exp_counts), (split, k, h, w, band)
-
-
-def test_small_board_picks_level_split(golhip, oracle):
-    """configs[1]-sized boards take the level-split path automatically; results unchanged."""
+def test_small_board_5120x512_vs_oracle(golhip, oracle):
+    """A configs[1]-wide short board on the automatic kernel choice, every count vs the oracle."""
     words = oracle.init_random(5120, 512, seed=2)
     with golhip.Engine(5120, 512, k=16) as e:
         e.load_words(words)
@@ -491,107 +436,22 @@ def test_small_board_picks_level_split(golhip, oracle):
 
 
 @pytest.mark.parametrize("k", [6, 16])
-def test_count_window_flushes(golhip, oracle, monkeypatch, k):
+def test_count_window_flushes(golhip, oracle, k):
     """Per-turn counts go through a count window finalized once per window: with the window at
     its 128-generation minimum and graphs off, a 700-turn call flushes it several times (K = 6
     does not divide it); every count must equal the oracle's and the board must match."""
-    monkeypatch.setenv("GOLHIP_COUNT_WINDOW", "128")
-    monkeypatch.setenv("GOLHIP_GRAPHS", "0")
     w, h = 640, 200
     board = oracle.unpack(oracle.init_random(640, h, seed=11), w)
     with golhip.Engine(w, h, k=k) as e:
+        e.step(20, counts=True)  # counts through the default window first, then resize it
+        e.set_count_window(128)
+        e.set_graphs(0)
         e.load(board)
         c = e.step(700, counts=True)
         got = e.store()
     exp, exp_counts = oracle.packed_run(board, 700)
     assert np.array_equal(got, exp)
     assert np.array_equal(c.astype(np.int64), exp_counts)  # exp_counts[i]: after turn i + 1
-
-
-TILE_CONFIGS = [(2, 16), (4, 8), (4, 16), (4, 32), (6, 16), (8, 8), (8, 16), (8, 32), (10, 16),
-                (12, 8), (12, 16), (12, 32), (14, 16), (16, 8), (16, 16), (16, 32)]
-
-
-@pytest.mark.parametrize("k,tile", TILE_CONFIGS)
-def test_register_tile_kernel(golhip, oracle, monkeypatch, k, tile):
-    """The register-tile stencil (gol_tile: T + 2K rows of a 62-word chunk in VGPRs, K
-    generations in place) forced at every compiled (K, T): wrap in both directions, boards
-    shorter than a tile and than its halo, ragged widths, short last tiles, per-turn counts."""
-    monkeypatch.setenv("GOLHIP_TILE", str(tile))
-    for (h, w) in [(77, 640), (16, 16), (5, 96), (300, 4160), (129, 200), (40, 8192), (64, 1984)]:
-        rng = np.random.default_rng(h * 7 + w + k + tile)
-        board = ((rng.random((h, w)) < 0.4) * 255).astype(np.uint8)
-        turns = 3 * k + 1
-        exp, exp_counts = oracle.packed_run(board, turns)
-        out, counts, _, _ = run_engine(golhip, board, turns, k=k, counts=True)
-        assert np.array_equal(out, exp), (k, tile, h, w)
-        assert np.array_equal(counts.astype(np.int64), exp_counts), (k, tile, h, w)
-
-
-@pytest.mark.parametrize("k", [4, 16])
-def test_register_tile_tracked_flips(golhip, oracle, monkeypatch, k):
-    """Flips tracking through the tile kernel: the last launch's LD instantiation writes the last
-    generation's flips beside its output."""
-    monkeypatch.setenv("GOLHIP_TILE", "16")
-    h, w = 300, 640
-    rng = np.random.default_rng(k)
-    board = ((rng.random((h, w)) < 0.4) * 255).astype(np.uint8)
-    turns = 2 * k + 1
-    before, _ = oracle.packed_run(board, turns - 1)
-    exp, _ = oracle.packed_run(board, turns)
-    with golhip.Engine(w, h, k=k) as e:
-        e.set_fixed_k(True)
-        e.track_flips(True)
-        e.load(board)
-        e.step(turns)
-        assert e.launch_kind(k) == ("tile", 16)
-        got = [tuple(c) for c in e.flips().tolist()]
-        assert np.array_equal(e.store(), exp)
-    assert got == oracle.flips(before, exp)
-
-
-SLAB_CONFIGS = [(8, 8, 4), (8, 8, 8), (12, 8, 8), (16, 8, 8), (16, 8, 12), (16, 16, 8),
-                (16, 8, 12, 2), (16, 12, 8, 2), (16, 12, 8), (16, 12, 7, 2), (16, 10, 8, 2),
-                (16, 14, 6, 2)]
-
-
-@pytest.mark.parametrize("cfg", SLAB_CONFIGS)
-def test_register_slab_kernel(golhip, oracle, monkeypatch, cfg):
-    """The register-slab stencil (gol_slab: W waves x S rows of a 62-word chunk in VGPRs, edge
-    rows swapped through LDS every generation) forced at every compiled (K, W, S): wrap, boards
-    shorter than a slab, ragged widths, short last slabs, per-turn counts."""
-    k, waves, rows = cfg[:3]
-    code = (cfg[3] * 10000 if len(cfg) > 3 else 0) + waves * 100 + rows
-    monkeypatch.setenv("GOLHIP_SLAB", str(code))
-    for (h, w) in [(77, 640), (16, 16), (5, 96), (300, 4160), (129, 200), (40, 8192), (250, 1984),
-                   (100, 4096)]:
-        rng = np.random.default_rng(h * 7 + w + k + waves + rows)
-        board = ((rng.random((h, w)) < 0.4) * 255).astype(np.uint8)
-        turns = 3 * k + 1
-        exp, exp_counts = oracle.packed_run(board, turns)
-        with golhip.Engine(w, h, k=k) as e:
-            assert e.launch_kind(k) == ("slab", code)
-        out, counts, _, _ = run_engine(golhip, board, turns, k=k, counts=True)
-        assert np.array_equal(out, exp), (k, waves, rows, h, w)
-        assert np.array_equal(counts.astype(np.int64), exp_counts), (k, waves, rows, h, w)
-
-
-def test_register_slab_tracked_flips(golhip, oracle, monkeypatch):
-    monkeypatch.setenv("GOLHIP_SLAB", "1608")
-    h, w, k = 300, 640, 16
-    rng = np.random.default_rng(5)
-    board = ((rng.random((h, w)) < 0.4) * 255).astype(np.uint8)
-    turns = 2 * k + 1
-    before, _ = oracle.packed_run(board, turns - 1)
-    exp, _ = oracle.packed_run(board, turns)
-    with golhip.Engine(w, h, k=k) as e:
-        e.set_fixed_k(True)
-        e.track_flips(True)
-        e.load(board)
-        e.step(turns)
-        got = [tuple(c) for c in e.flips().tolist()]
-        assert np.array_equal(e.store(), exp)
-    assert got == oracle.flips(before, exp)
 
 
 def test_small_board_picks_register_slab(golhip, oracle):
