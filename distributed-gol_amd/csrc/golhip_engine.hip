@@ -133,7 +133,13 @@ struct golhip_engine {
     // the next exchange sends, so with K' <= edge_k that exchange waits only for those bands
     int edge_k = 0;
     std::string comm_pending;  // the last RCCL operation enqueued (rank, peers, K, bytes)
-    int test_recv_extra_rows = 0;  // GOLHIP_RING_SELF=2: the top-halo receive posts K + 1 rows
+    // GOLHIP_RING_SELF test modes: 2 = the first send of every exchange is never posted (its
+    // receive has no match), 3 = the comm stream stalls 20 s behind each exchange (a peer whose
+    // halos never arrive in time: the boundary bands and everything after them stay pending)
+    int test_ring_mode = 1;
+    // tuning build, GOLHIP_VARIANT=stamp: per-wave timestamps of the last single-strip launch
+    uint64_t *stamp_buf = nullptr;
+    int64_t stamp_waves = 0;
     std::vector<Shard> shards;
     int cur = 0;
     bool prev_valid = false;
@@ -260,8 +266,10 @@ int wait_stream(golhip_t h, hipStream_t st) {
 int comm_ready(golhip_t h, ncclComm_t c, const char *what) {
     return poll_until(h, what, [&]() -> int {
         ncclResult_t st = ncclSuccess;
-        if (ncclCommGetAsyncError(c, &st) != ncclSuccess) return 0;
-        return st == ncclInProgress ? 1 : 0;  // errors are taken by poll_until
+        const ncclResult_t q = ncclCommGetAsyncError(c, &st);
+        if (q != ncclSuccess) return comm_abort(h, what, q);
+        if (st == ncclInProgress) return 1;
+        return st == ncclSuccess ? 0 : comm_abort(h, what, st);
     });
 }
 
@@ -466,6 +474,7 @@ int setup_engine(golhip_t h, int width, int height, int world, int k) {
                      : std::strcmp(e, "driftlds") == 0 ? golhip::kVariantDriftLds
                      : std::strcmp(e, "pre63") == 0 ? golhip::kVariantPre63
                      : std::strcmp(e, "prodmask") == 0 ? golhip::kVariantProdMask
+                     : std::strcmp(e, "stamp") == 0 ? golhip::kVariantStamp
                                                        : golhip::kVariantProd;  // prod
 #endif
     return GOLHIP_OK;
@@ -725,11 +734,16 @@ RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K, bool counting) 
     struct Cand {
         int W, S, NC;
     };
-    static constexpr Cand kCount16[] = {{8, 12, 2}, {12, 8, 2}, {12, 7, 2}};
-    static constexpr Cand kPlain16[] = {{8, 12, 2}, {12, 7, 2}};
+    // Round 4: gol_slab2 (NC = 9, the edge hand-off off the critical path) at K = 16, in the
+    // measured order of the model's ties (profiles/r04/r04c_tune_slab.log, 4096 turns, every count
+    // checked): with counts 8 x 12 0.843 / 16 x 6 0.844 / 12 x 8 0.856 us/turn at 5120^2, without
+    // counts 16 x 6 0.735 / 12 x 8 0.744 / 8 x 12 0.790; 4096^2 takes 12 x 7 either way (0.781 /
+    // 0.662: 237 slabs, 21 rows per SIMD).
+    static constexpr Cand kCount16[] = {{8, 12, 9}, {16, 6, 9}, {12, 8, 9}, {12, 7, 9}};
+    static constexpr Cand kPlain16[] = {{16, 6, 9}, {12, 8, 9}, {8, 12, 9}, {12, 7, 9}};
     static constexpr Cand kOther[] = {{8, 8, 4}};
     const Cand *cands = K == 16 ? (counting ? kCount16 : kPlain16) : kOther;
-    const int ncand = K == 16 ? (counting ? 3 : 2) : 1;
+    const int ncand = K == 16 ? 4 : 1;
     double best = 1e300;
     for (int i = 0; i < ncand; ++i) {
         const Cand c = cands[i];
@@ -925,17 +939,18 @@ int exchange_halos(golhip_t h, int K) {
             const golhip_xfer &x = plan[i];
             uint32_t *p = r0 + x.row * h->pitch;
             if (x.kind == 0) {
+                if (i == 0 && h->test_ring_mode == 2) continue;  // test hook: an unmatched receive
                 NCCLCALL(h, "ncclSend", ncclSend(p, bytes, ncclUint8, x.peer, s.comm_nccl, s.comm));
             } else {
-                // test hook (GOLHIP_RING_SELF=2): the top-halo receive (rows -K .. 0, in bounds)
-                // asks for one row more than the matching send delivers
-                const size_t rb = bytes + (i == 2 ? (size_t)h->test_recv_extra_rows * h->pitch * 4 : 0);
-                NCCLCALL(h, "ncclRecv", ncclRecv(p, rb, ncclUint8, x.peer, s.comm_nccl, s.comm));
+                NCCLCALL(h, "ncclRecv", ncclRecv(p, bytes, ncclUint8, x.peer, s.comm_nccl, s.comm));
             }
         }
         NCCLCALL(h, "ncclGroupEnd", ncclGroupEnd());
         int rc = comm_ready(h, s.comm_nccl, "the halo exchange's RCCL group");
         if (rc) return rc;
+        if (h->test_ring_mode == 3)  // test hook: the halos land 20 s late (a stalled peer)
+            HIPCHK(h, hipLaunchHostFunc(
+                          s.comm, [](void *) { std::this_thread::sleep_for(std::chrono::seconds(20)); }, nullptr));
     } else {
         const int n = (int)h->shards.size();
         for (int i = 0; i < n; ++i) {
@@ -987,6 +1002,10 @@ int step_block(golhip_t h, int K, int64_t slot_gen, int64_t diff_slot = kDiffNon
         if (!h->split) {
             StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0, 0, slots != nullptr);
             p.diff = diff;
+            if (h->stamp_buf && !diff) {  // tuning: the stamp variant writes p.diff as its stamps
+                p.diff = reinterpret_cast<uint32_t *>(h->stamp_buf);
+                h->stamp_waves = p.nbands * (int64_t)p.nchunks;
+            }
             // a K-deep ring launch (ring_depth: a production register slab) writes the flips of
             // each of its K generations into K consecutive ring slots
             p.diff_stride = diff_slot >= 0 && K > 1 ? s.rows * h->pitch : 0;
@@ -1215,7 +1234,13 @@ int transfer_bytes(golhip_t h, uint8_t *host, size_t row_stride, bool to_device)
     return GOLHIP_OK;
 }
 
+constexpr int64_t kStampWaves = 1 << 20;
+
 int create_common(golhip_t h) {
+    if (h->variant == golhip::kVariantStamp) {
+        HIPCHK(h, hipSetDevice(h->shards[0].device));
+        HIPCHK(h, hipMalloc(&h->stamp_buf, sizeof(uint64_t) * 4 * kStampWaves));
+    }
     for (auto &s : h->shards) {
         int rc = alloc_shard(h, s);
         if (rc) return rc;
@@ -1442,13 +1467,13 @@ int golhip_create_rank(int width, int height, int rank, int world_size, int devi
     h->rank_mode = true;
     // Test hook: GOLHIP_RING_SELF=1 makes a world-1 rank engine a ring of ONE halo'd strip whose
     // halos go through RCCL send/recv to itself, so the whole rank-mode path (plan, RCCL group,
-    // interior/boundary overlap, count all-reduce) runs on a one-GPU box.  GOLHIP_RING_SELF=2:
-    // the same ring, whose top-halo receive asks for one row more than the matching send delivers
-    // -- an exchange that cannot complete as posted, for the fail-fast test (tests/test_gpu_failfast.py).
+    // interior/boundary overlap, count all-reduce) runs on a one-GPU box.  GOLHIP_RING_SELF=2 / 3:
+    // the same ring with an unmatched receive / a comm stream stalled behind a host function, for
+    // the fail-fast tests (tests/test_gpu_failfast.py).
     if (ring_self) {
         h->split = true;
         h->halo = k;
-        h->test_recv_extra_rows = std::atoi(rs) == 2 ? 1 : 0;
+        h->test_ring_mode = std::atoi(rs);
     }
     h->shards.resize(1);
     Shard &s = h->shards[0];
@@ -1550,9 +1575,27 @@ int golhip_destroy(golhip_t h) {
     for (auto &s : h->shards) free_shard(s, rccl_waits(h) ? h->comm_timeout_ms : 0);
     for (void *b : h->hc_buf)
         if (b) (void)hipHostFree(b);
+    if (h->stamp_buf) (void)hipFree(h->stamp_buf);
     delete h;
     return GOLHIP_OK;
 }
+
+#ifdef GOLHIP_TUNING
+// Tuning build only (not in include/golhip.h): the per-wave stamps of the last single-strip
+// launch of a GOLHIP_VARIANT=stamp handle, 4 uint64 per wave (start, end: s_memrealtime 100 MHz;
+// shader cycles; HW_ID | XCC_ID << 32).  scripts/stamp_launch.py.
+int golhip_tuning_stamps(golhip_t h, uint64_t *out, size_t cap_waves, size_t *n_waves) {
+    if (!h || !n_waves) return GOLHIP_ERR_ARG;
+    if (!h->stamp_buf) return fail(h, GOLHIP_ERR_STATE, "not a GOLHIP_VARIANT=stamp handle");
+    int rc = sync_all(h);
+    if (rc) return rc;
+    *n_waves = (size_t)std::min<int64_t>(h->stamp_waves, kStampWaves);
+    if (!out) return GOLHIP_OK;
+    if (cap_waves < *n_waves) return GOLHIP_ERR_CAP;
+    HIPCHK(h, hipMemcpy(out, h->stamp_buf, sizeof(uint64_t) * 4 * *n_waves, hipMemcpyDeviceToHost));
+    return GOLHIP_OK;
+}
+#endif
 
 const char *golhip_last_error(golhip_t h) { return h ? h->err.c_str() : g_create_error.c_str(); }
 
@@ -2122,7 +2165,7 @@ int golhip_launch_plan(int64_t width, int64_t height, int strips, int k, int64_t
     const int64_t per = golhip::chunk_words(Kfull, golhip::kVariantProd);
     const int64_t waves1 = (height + std::max(Kfull, 8) - 1) / std::max(Kfull, 8) * ((wd + per - 1) / per);
     const bool stream = strips > 1 || !golhip::stencil_slab_supported(Kfull, 8, Kfull == 16 ? 12 : 8,
-                                                                       Kfull == 16 ? 2 : 4) ||
+                                                                       Kfull == 16 ? 9 : 4) ||
                         waves1 > 16 * 256;
     LaunchPlanner plan(strip_cells, k, turns, strips == 1 && small_board(cells, Kfull), false, false,
                        4096, stream);

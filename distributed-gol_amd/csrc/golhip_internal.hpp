@@ -83,7 +83,10 @@ constexpr int kVariantProd = 12;
 constexpr int kVariantPre63 = 13;
 // production with the lanes of the last column chunk that nothing depends on exec-masked off
 constexpr int kVariantProdMask = 14;
-constexpr int kNumVariants = 15;
+// production with per-wave timestamps (tuning build: dispatch skew, wave durations, per-SIMD
+// tails and the in-kernel clock of a launch; golhip_tuning_stamps)
+constexpr int kVariantStamp = 15;
+constexpr int kNumVariants = 16;
 // The pre-shifted geometry in production: every non-counting launch of depth 2..16 (the driver's
 // dense 20-turn region, pre-heated: +1.2 % over the 62-word chunks, profiles/r03/r03aa_ab_split.log;
 // K = 16 +2.9 %), and counting launches at K = 16 only (with counts at K < 16 its allocator holds
@@ -93,7 +96,7 @@ constexpr bool prod_pre(int K, bool counting = false) { return K == 16 || (!coun
 inline bool variant_is_production_family(int v) {
     return v == kVariantChainLdsPf || v == kVariantDriftLds || v == kVariantDriftZip ||
            v == kVariantDrift62 || v == kVariantDriftNoFill || v == kVariantProd || v == kVariantPre63 ||
-           v == kVariantProdMask;
+           v == kVariantProdMask || v == kVariantStamp;
 }
 inline int variant_words(int v) {
     return (v == kVariantSkewD2 || v == kVariantChainD2 || v == kVariantSkewLdsD2 ||
@@ -109,7 +112,8 @@ inline int chunk_words(int K, int variant, bool counting = false) {
         return 256;  // gol_step1: 4 words x 64 lanes
     const int d = variant_words(variant);
     if (variant == kVariantDriftZip || variant == kVariantDrift62) return 62;
-    if (variant == kVariantProd || variant == kVariantProdMask) return prod_pre(K, counting) ? 63 : 62;
+    if (variant == kVariantProd || variant == kVariantProdMask || variant == kVariantStamp)
+        return prod_pre(K, counting) ? 63 : 62;
     if (variant == kVariantPre63) return K <= 16 ? 63 : 62;
     return (d == 1 && K <= 16) ? 63 : 62 * d;
 }

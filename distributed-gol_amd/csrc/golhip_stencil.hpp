@@ -384,8 +384,13 @@ __device__ __forceinline__ void flush_counts(const uint32_t (&acc)[NL], int j0, 
 // MASK = true: lanes no output or count depends on (past the row end in the last column chunk:
 //             at 65536 wide its 62-word chunk holds 2 words) run the launch exec-masked off, so
 //             they issue nothing into the datapath; the wave's instruction stream is unchanged.
+// STAMP = true (tuning build, kVariantStamp): lane 0 of every wave writes its start and end
+//             (s_memrealtime, 100 MHz), its shader-clock cycles (s_memtime delta) and its
+//             HW_ID / XCC_ID to ((uint64_t *)p.diff)[4 wave ..]: the launch's dispatch skew,
+//             wave durations, per-SIMD tails and in-kernel clock (scripts/stamp_launch.py).
 template <int K, bool COUNT, bool SKEW, int D, int PF, bool HH, bool DR = false, int ZIP = 1,
-          bool FILLU = true, bool LD = false, int WPE = 0, bool PRE = false, bool MASK = false>
+          bool FILLU = true, bool LD = false, int WPE = 0, bool PRE = false, bool MASK = false,
+          bool STAMP = false>
 // (PRE with counts at K = 16 (production): left alone, the allocator spends 224 VGPRs, i.e. 2 waves
 // per SIMD; held to the half-word-halo kernel's 3 it needs 142 and no scratch.  At K = 12, 4 waves
 // would spill: no hint there.)
@@ -406,6 +411,11 @@ void gol_stencil(const uint32_t *__restrict__ in,
     const int64_t chunk = wave % p.nchunks;
     const int64_t bandi = wave / p.nchunks;
     if (bandi >= p.nbands) return;  // wave-uniform
+    uint64_t stamp_t0 = 0, stamp_c0 = 0;
+    if constexpr (STAMP) {
+        stamp_t0 = __builtin_amdgcn_s_memrealtime();
+        stamp_c0 = __builtin_amdgcn_s_memtime();
+    }
     int ya, yb;
     band_rows(p, bandi, ya, yb);
     // First word (unwrapped) of this lane and its wrapped column.
@@ -768,6 +778,18 @@ void gol_stencil(const uint32_t *__restrict__ in,
         }
         flush_counts<K>(acc, 0, lane, wave, slots);
     }
+    if constexpr (STAMP) {
+        const uint64_t t1 = __builtin_amdgcn_s_memrealtime(), c1 = __builtin_amdgcn_s_memtime();
+        const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+        const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+        if (lane == 0) {
+            uint64_t *st = reinterpret_cast<uint64_t *>(p.diff) + 4 * wave;
+            st[0] = stamp_t0;
+            st[1] = t1;
+            st[2] = c1 - stamp_c0;
+            st[3] = (uint64_t)hw | ((uint64_t)xcc << 32);
+        }
+    }
 }
 
 // ---------------------------------------------------------------- one generation (K = 1)
@@ -1096,13 +1118,22 @@ inline const void *step1_fn() {
 #endif
 
 template <int K, bool SKEW, int D, int PF = 0, bool DR = false, int ZIP = 1, bool HH = kHalfHalo<K, D>,
-          bool FILLU = true, bool ALLOW_LD = false, bool PRE = false, bool MASK = false>
+          bool FILLU = true, bool ALLOW_LD = false, bool PRE = false, bool MASK = false, bool STAMP = false>
 hipError_t launch_stencil_k(const uint32_t *in, uint32_t *out, const StencilParams &p,
                             unsigned long long *slots, hipStream_t s) {
     const int64_t waves = p.nbands * (int64_t)p.nchunks;
     // at least one block: an empty launch (nbands = 0, every wave returns at once) is how
     // warm_stencil_k loads this depth's code object before anything is timed
     const unsigned blocks = (unsigned)std::max<int64_t>(1, (waves + 3) / 4);
+    if constexpr (STAMP) {  // p.diff is the stamp buffer (no flips in this variant)
+        if (slots)
+            hipLaunchKernelGGL((gol_stencil<K, true, SKEW, D, PF, HH, DR, ZIP, FILLU, false, 0, PRE, MASK, true>),
+                               dim3(blocks), dim3(256), lds_pad_bytes(), s, in, out, p, slots);
+        else
+            hipLaunchKernelGGL((gol_stencil<K, false, SKEW, D, PF, HH, DR, ZIP, FILLU, false, 0, PRE, MASK, true>),
+                               dim3(blocks), dim3(256), lds_pad_bytes(), s, in, out, p, slots);
+        return hipGetLastError();
+    }
     if (p.diff) {  // last-generation flips beside the output (production variants only)
         if constexpr (ALLOW_LD) {
             if (slots)
@@ -1179,6 +1210,13 @@ hipError_t launch_variant(int variant, const uint32_t *in, uint32_t *out, const 
             else return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true>(in, out, p, slots, s);
         case kVariantProd:  // per depth and counting: the fastest measured (golhip_internal.hpp)
             return launch_prod<K>(in, out, p, slots, s);
+        case kVariantStamp:  // the production kernel with per-wave timestamps (p.diff: stamps)
+            if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
+            else if constexpr (K <= 16) {
+                if (prod_pre(K, slots != nullptr))
+                    return launch_stencil_k<K, false, 1, 1, true, 1, false, true, false, true, false, true>(in, out, p, slots, s);
+                return launch_stencil_k<K, false, 1, 1, true, 1, false, true, false, false, false, true>(in, out, p, slots, s);
+            } else return launch_stencil_k<K, false, 1, 1, true, 1, false, true, false, false, false, true>(in, out, p, slots, s);
         case kVariantDriftNoFill:
             if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
             else return launch_stencil_k<K, false, 1, 1, (K <= 16), 1, kHalfHalo<K, 1>, false>(in, out, p, slots, s);
@@ -1219,6 +1257,10 @@ const void *variant_fn(int variant) {
             if constexpr (K == 1) return step1_fn();
             else return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1>;
         case kVariantProd: return prod_fn<K>();
+        case kVariantStamp:
+            if constexpr (K == 1) return step1_fn();
+            else if constexpr (prod_pre(K)) return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1, true, false, 0, true, false, true>;
+            else return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1, true, false, 0, false, false, true>;
         case kVariantDriftNoFill:
             if constexpr (K == 1) return step1_fn();
             else return (const void *)gol_stencil<K, false, false, 1, 1, kHalfHalo<K, 1>, (K <= 16), 1, false>;

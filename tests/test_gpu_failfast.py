@@ -5,8 +5,10 @@ Broker.Publish forever, broker/broker.go:58-84).
 
 Each case runs in a FRESH process under its own time limit, so a failure of the deadline itself
 ends in a killed child, not a hung test session:
-  * exchange: the ring-of-one hook GOLHIP_RING_SELF=2 posts a top-halo receive one row longer than
-    the matching send -- the K-row exchange can never complete as posted;
+  * unmatched receive: the ring-of-one hook GOLHIP_RING_SELF=2 never posts one send of each
+    exchange;
+  * stalled halos: GOLHIP_RING_SELF=3 holds the comm stream 20 s behind each exchange, so the
+    boundary bands and the sync wait on halos that do not arrive in time;
   * init: rank 0 of a 2-rank communicator whose rank 1 never joins -- ncclCommInitRankConfig
     (non-blocking) never finishes its set-up.
 """
@@ -31,6 +33,7 @@ case, timeout_ms = sys.argv[2], int(sys.argv[3])
 golhip.set_default_comm_timeout(timeout_ms)
 out = {"case": case}
 t0 = time.perf_counter()
+e = None
 try:
     if case == "exchange":
         e = golhip.Engine(640, 64, k=4, rank=0, world_size=1, device=0)
@@ -48,7 +51,7 @@ except golhip.GolHipError as err:
     out["msg"] = str(err)
 out["seconds"] = time.perf_counter() - t0
 t1 = time.perf_counter()
-if case == "exchange" and "code" in out:
+if case == "exchange" and "code" in out and e is not None:
     # the handle refuses further device work with the same error, and destroys without hanging
     try:
         e.step(1)
@@ -74,27 +77,49 @@ def run_child(case, timeout_ms, ring_self=None):
     return json.loads(lines[-1])
 
 
-def test_exchange_that_cannot_complete_fails_fast(golhip):
-    timeout_ms = 3000
-    t = time.perf_counter()
-    out = run_child("exchange", timeout_ms, ring_self="2")
-    assert out.get("halo_rows") == 4
+def check_exchange_failure(golhip, out, timeout_ms, within_s):
+    assert out.get("halo_rows") == 4, out  # created (the failure must come from the exchange)
     assert not out.get("completed"), out
     assert out["code"] == golhip.ERR_RCCL, out
-    # within the deadline (+ the modelled time of the queued work and a margin), not at a hang
-    assert out["seconds"] < timeout_ms / 1e3 + 20, out
+    assert out["seconds"] < within_s, out
     msg = out["msg"]
     # golhip_last_error names the rank, the pending operation, its peers, K and the byte count
     assert "rank 0 of 1" in msg and "K = 4" in msg and "bytes" in msg and "aborted" in msg, msg
     assert "<- rank 0" in msg and "-> rank 0" in msg, msg
-    assert out["after"] == golhip.ERR_RCCL, out
+    assert out["after"] == golhip.ERR_RCCL, out  # the handle refuses further device work
+
+
+def test_unmatched_receive_fails_with_rccl_error(golhip):
+    """GOLHIP_RING_SELF=2: the first send of each exchange is never posted.  RCCL either rejects
+    the group or its receive never completes; either way ERR_RCCL well inside the deadline.
+    (A receive LONGER than its send -- the first hook tried -- completes silently on the self
+    path: RCCL copies within one rank, profiles/r04/failfast.txt.)"""
+    timeout_ms = 3000
+    out = run_child("exchange", timeout_ms, ring_self="2")
+    print(json.dumps(out))
+    check_exchange_failure(golhip, out, timeout_ms, timeout_ms / 1e3 + 20)
     assert out["teardown_seconds"] < timeout_ms / 1e3 + 20, out
-    assert time.perf_counter() - t < 150
+
+
+def test_stalled_halos_fail_at_the_deadline(golhip):
+    """GOLHIP_RING_SELF=3: every exchange's halos land 20 s late (the comm stream is held behind
+    each exchange).  The sync polls against the 3 s deadline, aborts the communicator and returns
+    ERR_RCCL naming the pending exchange; destroy does not wait for the stalled stream.  The
+    abort itself may wait for the RCCL kernel queued behind the stall to start and see the abort
+    flag (a real stuck transfer is a kernel already spinning), hence the bound of the stall."""
+    timeout_ms = 3000
+    out = run_child("exchange", timeout_ms, ring_self="3")
+    print(json.dumps(out))
+    check_exchange_failure(golhip, out, timeout_ms, timeout_ms / 1e3 + 25)
+    assert out["seconds"] >= timeout_ms / 1e3 * 0.9, out  # it waited for the deadline
+    assert "did not complete within" in out["msg"], out["msg"]
+    assert out["teardown_seconds"] < timeout_ms / 1e3 + 25, out
 
 
 def test_peer_that_never_joins_fails_fast_at_create(golhip):
     timeout_ms = 3000
     out = run_child("init", timeout_ms)
+    print(json.dumps(out))
     assert not out.get("completed"), out
     assert out["code"] == golhip.ERR_RCCL, out
     assert out["seconds"] < timeout_ms / 1e3 + 30, out
