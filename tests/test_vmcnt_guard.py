@@ -161,3 +161,26 @@ def test_production_k16_object_passes():
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:]
     assert ", 0 failed" in r.stdout
+
+
+def test_backward_execz_is_skipped_only_when_the_loop_closes_elsewhere():
+    """A backward s_cbranch_execz to the steady loop's top is an early exit inside the loop when a
+    later branch closes the loop; with no such branch it is kept as the back edge and warned about
+    (advice r03: skipping every execz could pick the wrong loop)."""
+    code, _ = ring_kernel(K=8, HH=0)
+    top = next(t for _, ins, t in code if ins.startswith("s_cbranch_scc1"))
+    hand = {i for i, (_, ins, _) in enumerate(code) if cv.vmcnt(ins) not in (None, 0)}
+    base = cv.linearize(code, hand)
+    # an execz inside the loop, jumping back to its top; the scc1 back edge still closes the loop
+    i_exec = next(i for i, (a, ins, t) in enumerate(code) if a > top and ins.startswith("ds_read"))
+    a_exec = code[i_exec][0]
+    with_inner = code[:i_exec] + [(a_exec, "s_cbranch_execz 65001", top)] + code[i_exec + 1:]
+    cv.LINEARIZE_NOTES.clear()
+    assert cv.linearize(with_inner, hand) == base
+    assert cv.LINEARIZE_NOTES == []
+    # the loop closed ONLY by a backward execz (no scc1 back edge): kept as the back edge, warned
+    only_exec = [(a, "s_cbranch_execz 65001" if ins.startswith("s_cbranch_scc1") else ins, t)
+                 for a, ins, t in code]
+    cv.LINEARIZE_NOTES.clear()
+    assert cv.linearize(only_exec, hand) == base
+    assert len(cv.LINEARIZE_NOTES) == 1 and "kept as a loop back edge" in cv.LINEARIZE_NOTES[0]
