@@ -308,13 +308,19 @@ def chunk_digests(words) -> list[bytes]:
             for y in range(0, w.shape[0], DIGEST_CHUNK_ROWS)]
 
 
-def board_digest(eng: golhip.Engine, world: int) -> str | None:
-    """SHA-256 of the chunk digests of the whole board (every rank's strip, in row order), or None
-    when a strip does not start on a chunk boundary or the width is not a multiple of 64."""
+def strip_words(eng: golhip.Engine):
+    """This rank's strip as packed uint64 rows (a host copy, ~15 ms for 512 MiB), or None when it
+    cannot enter the board digest (width not a multiple of 64, strip not on a chunk boundary)."""
     info = eng.info
-    mine = None
     if info.width % 64 == 0 and info.y0 % DIGEST_CHUNK_ROWS == 0:
-        mine = chunk_digests(eng.store_words())
+        return eng.store_words()
+    return None
+
+
+def board_digest(words, world: int) -> str | None:
+    """SHA-256 of the chunk digests of the whole board (every rank's strip_words, in row order), or
+    None when a strip could not be hashed.  Collective at world > 1."""
+    mine = chunk_digests(words) if words is not None else None
     if world > 1:
         parts = [None] * world
         dist.all_gather_object(parts, mine)
@@ -545,16 +551,20 @@ def main():
     # regression canary: alive cells after exactly warmup + steps generations (deterministic for
     # the seed; compare across kernel versions)
     alive_timed = eng.alive_count()
-    # the whole board after the timed pass, bit for bit: every rank hashes its strip in 4096-row
-    # chunks (outside the timed region), rank 0 hashes the gathered chunk digests
-    digest = board_digest(eng, world)
+    # the whole board after the timed pass, bit for bit: every rank copies its strip to the host
+    # now (outside the timed region) and hashes it in 4096-row chunks after the instrumented pass
+    # (a second of host hashing here would let the chip's clock drop before that pass)
+    timed_words = strip_words(eng)
     instrumented = None
     if a.no_timing:
         launches = -(-a.steps // a.k)
         kern_ms, gens = dt * 1e3, a.steps
     else:
         # roofline pass: the same warmup + timed turns from the seed again, with per-launch HIP
-        # events on the compute stream (every rank: the steps exchange halos when N > 1)
+        # events on the compute stream (every rank: the steps exchange halos when N > 1); a short
+        # re-heat first (the host copy above idled the GPU), the same turn count on every rank
+        if cold is not None:
+            eng.step(max(a.k, cold["preheat_turns"] // 4 // a.k * a.k))
         eng.init_random(a.seed)
         eng.step(a.warmup)
         eng.sync()
@@ -572,6 +582,8 @@ def main():
                         "kernel_ms": round(kern_ms, 4), "launches": launches,
                         "note": "the same warmup + timed turns from the seed, with per-launch HIP "
                                 "events (roofline.avg_launch_us); value is the uninstrumented pass"}
+    digest = board_digest(timed_words, world)
+    del timed_words
     total_updates = width * height * a.steps
     gcups = total_updates / dt / 1e9
     ms_per_step = dt * 1e3 / a.steps
@@ -838,4 +850,8 @@ if __name__ == "__main__":
         calls = ", ".join(f"{getattr(x, 'last_call', '?')}" for x in ENGINES) or "none"
         print(f"bench: rank {rank} failed: {e!r}; last engine call(s): {calls}", file=sys.stderr,
               flush=True)
-        raise SystemExit(3)
+        sys.stdout.flush()
+        # no interpreter teardown: after an RCCL failure the engine's communicator is left in
+        # place with work possibly queued behind a stuck transfer (golhip_engine.hip comm_abort);
+        # ending the process is what removes it
+        os._exit(3)

@@ -38,6 +38,7 @@ constexpr int kVersion = 101;
 // least the graph length kGraphGens: tests shrink it to exercise flushes).
 constexpr int kCountWindowDefault = 4096;
 constexpr int kCountWindowMin = 128;
+constexpr int64_t kStampWaves = 1 << 20;  // tuning build: waves of the per-wave stamp buffer
 // Default deadline of a host wait on RCCL-dependent work and of the communicator's set-up
 // (golhip_set_comm_timeout(NULL, ms) changes it for later creates): well under the 600 s a driver
 // gives a whole bench run, far above any legitimate wait (an 8-rank init takes seconds, a K-row
@@ -128,14 +129,14 @@ struct golhip_engine {
     int64_t comm_timeout_ms = 0;
     double queued_s = 0.0;  // modelled seconds of stencil work queued since the last full sync
     bool comm_failed = false;
+    bool comm_setup_done = false;  // the communicator's set-up completed (no abort after it)
     // depth of the boundary bands the last split block ran on the edge stream (0: none, e.g. a strip
     // shorter than 3K or a non-split launch): its rows [0, K) and [rows - K, rows) are exactly what
     // the next exchange sends, so with K' <= edge_k that exchange waits only for those bands
     int edge_k = 0;
     std::string comm_pending;  // the last RCCL operation enqueued (rank, peers, K, bytes)
-    // GOLHIP_RING_SELF test modes: 2 = the first send of every exchange is never posted (its
-    // receive has no match), 3 = the comm stream stalls 20 s behind each exchange (a peer whose
-    // halos never arrive in time: the boundary bands and everything after them stay pending)
+    // GOLHIP_RING_SELF=2 (test hook): every step's work ends in a 20 s stall of the compute stream
+    // (a rank whose device work does not finish in time); nothing RCCL is queued behind it
     int test_ring_mode = 1;
     // tuning build, GOLHIP_VARIANT=stamp: per-wave timestamps of the last single-strip launch
     uint64_t *stamp_buf = nullptr;
@@ -191,19 +192,30 @@ int fail(golhip_t h, int code, const char *fmt, ...) {
 // the all-reduce).  Only then do host waits poll; everything else synchronises directly.
 bool rccl_waits(golhip_t h) { return h->rank_mode && h->split && !h->host_comm_on; }
 
-// Abort the communicator (its kernels see the abort flag and return) and fail the call with the
-// pending operation named.  The handle stays unusable for device work afterwards (comm_failed).
+// Fail the call with the pending operation named; the handle refuses device work afterwards
+// (comm_failed).  Before the communicator's set-up has completed nothing of it runs on the device,
+// and ncclCommAbort stops its bootstrap.  After it, the communicator is NOT aborted: ncclCommAbort
+// frees its device state while RCCL kernels queued on this rank's streams behind the stuck one may
+// still run -- measured on the one-GPU box, an abort with exchanges queued behind a stalled comm
+// stream left the GPU with a memory-access fault (profiles/r04/failfast.txt).  The communicator
+// and the strips are left in place (golhip_destroy leaks what a stuck stream may still touch) and
+// the caller is expected to end the process (bench.py exits at once); the process teardown
+// removes its queues.
 int comm_abort(golhip_t h, const char *why, ncclResult_t state) {
-    for (auto &s : h->shards)
-        if (s.comm_nccl) {
-            (void)ncclCommAbort(s.comm_nccl);
-            s.comm_nccl = nullptr;
-        }
+    const bool before_setup = !h->comm_setup_done;
+    if (before_setup)
+        for (auto &s : h->shards)
+            if (s.comm_nccl) {
+                (void)ncclCommAbort(s.comm_nccl);
+                s.comm_nccl = nullptr;
+            }
     h->comm_failed = true;
-    return fail(h, GOLHIP_ERR_RCCL, "rank %d of %d: %s: %s (communicator state: %s); communicator aborted",
+    return fail(h, GOLHIP_ERR_RCCL, "rank %d of %d: %s: %s (communicator state: %s); %s",
                 h->shards.empty() ? -1 : h->shards[0].rank, h->world_size, why,
                 h->comm_pending.empty() ? "no RCCL operation pending" : h->comm_pending.c_str(),
-                ncclGetErrorString(state));
+                ncclGetErrorString(state),
+                before_setup ? "communicator aborted"
+                             : "communicator left in place, end the process (RCCL work may still be queued)");
 }
 
 using Clock = std::chrono::steady_clock;
@@ -245,8 +257,7 @@ int poll_until(golhip_t h, const char *what, F &&done) {
 // hipStreamSynchronize, bounded by the RCCL deadline in rank mode.
 int wait_stream(golhip_t h, hipStream_t st) {
     if (h->comm_failed)
-        return fail(h, GOLHIP_ERR_RCCL, "the communicator was aborted by an earlier failure: %s",
-                    h->comm_pending.c_str());
+        return fail(h, GOLHIP_ERR_RCCL, "the communicator failed earlier: %s", h->comm_pending.c_str());
     if (!rccl_waits(h)) {
         const hipError_t e = hipStreamSynchronize(st);
         if (e != hipSuccess)
@@ -335,8 +346,13 @@ constexpr int64_t kStageBytes = 64ll << 20;
 int alloc_shard(golhip_t h, Shard &s) {
     HIPCHK(h, hipSetDevice(s.device));
     HIPCHK(h, hipStreamCreateWithFlags(&s.compute, hipStreamNonBlocking));
-    HIPCHK(h, hipStreamCreateWithFlags(&s.comm, hipStreamNonBlocking));
-    HIPCHK(h, hipStreamCreateWithFlags(&s.edge, hipStreamNonBlocking));
+    // the halo exchange and the boundary bands are short and on the critical path of a split
+    // board's block (the next exchange waits for the bands): their streams get the device's highest
+    // priority, so their few workgroups are dispatched ahead of the interior's waiting ones
+    int lo_prio = 0, hi_prio = 0;
+    HIPCHK(h, hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
+    HIPCHK(h, hipStreamCreateWithPriority(&s.comm, hipStreamNonBlocking, hi_prio));
+    HIPCHK(h, hipStreamCreateWithPriority(&s.edge, hipStreamNonBlocking, hi_prio));
     HIPCHK(h, hipEventCreateWithFlags(&s.ev_ready, hipEventDisableTiming));
     HIPCHK(h, hipEventCreateWithFlags(&s.ev_halo, hipEventDisableTiming));
     HIPCHK(h, hipEventCreateWithFlags(&s.ev_edge, hipEventDisableTiming));
@@ -367,7 +383,7 @@ int alloc_shard(golhip_t h, Shard &s) {
 // drain_ms > 0 (a handle whose work can wait on RCCL): wait at most that long for the streams; a
 // stream still busy after it (an RCCL transfer nothing will ever match) is left to the process's
 // teardown, and its memory is not freed under it.
-void free_shard(Shard &s, int64_t drain_ms = 0) {
+void free_shard(Shard &s, int64_t drain_ms = 0, bool comm_failed = false) {
     (void)hipSetDevice(s.device);
     bool drained = true;
     for (hipStream_t st : {s.compute, s.comm, s.edge}) {
@@ -382,12 +398,8 @@ void free_shard(Shard &s, int64_t drain_ms = 0) {
             std::this_thread::sleep_for(std::chrono::microseconds(200));
         drained = drained && e != hipErrorNotReady;
     }
-    if (s.comm_nccl) {
-        if (drained)
-            (void)ncclCommDestroy(s.comm_nccl);
-        else
-            (void)ncclCommAbort(s.comm_nccl);
-    }
+    // a failed communicator is left alone (comm_abort); a stuck stream keeps what it may touch
+    if (s.comm_nccl && drained && !comm_failed) (void)ncclCommDestroy(s.comm_nccl);
     if (!drained) {
         s = Shard{};
         return;
@@ -911,8 +923,7 @@ int exchange_halos(golhip_t h, int K) {
                                          hipMemcpyHostToDevice, s.comm));
     } else if (h->rank_mode) {
         if (h->comm_failed)
-            return fail(h, GOLHIP_ERR_RCCL, "the communicator was aborted by an earlier failure: %s",
-                        h->comm_pending.c_str());
+            return fail(h, GOLHIP_ERR_RCCL, "the communicator failed earlier: %s", h->comm_pending.c_str());
         // Early exchange: the rows this exchange sends are the last block's boundary bands (edge
         // stream), done long before its interior -- so the transfer overlaps the previous block's
         // interior and the boundary bands of this block find their halos already in place.  The
@@ -939,7 +950,6 @@ int exchange_halos(golhip_t h, int K) {
             const golhip_xfer &x = plan[i];
             uint32_t *p = r0 + x.row * h->pitch;
             if (x.kind == 0) {
-                if (i == 0 && h->test_ring_mode == 2) continue;  // test hook: an unmatched receive
                 NCCLCALL(h, "ncclSend", ncclSend(p, bytes, ncclUint8, x.peer, s.comm_nccl, s.comm));
             } else {
                 NCCLCALL(h, "ncclRecv", ncclRecv(p, bytes, ncclUint8, x.peer, s.comm_nccl, s.comm));
@@ -948,9 +958,6 @@ int exchange_halos(golhip_t h, int K) {
         NCCLCALL(h, "ncclGroupEnd", ncclGroupEnd());
         int rc = comm_ready(h, s.comm_nccl, "the halo exchange's RCCL group");
         if (rc) return rc;
-        if (h->test_ring_mode == 3)  // test hook: the halos land 20 s late (a stalled peer)
-            HIPCHK(h, hipLaunchHostFunc(
-                          s.comm, [](void *) { std::this_thread::sleep_for(std::chrono::seconds(20)); }, nullptr));
     } else {
         const int n = (int)h->shards.size();
         for (int i = 0; i < n; ++i) {
@@ -1002,7 +1009,12 @@ int step_block(golhip_t h, int K, int64_t slot_gen, int64_t diff_slot = kDiffNon
         if (!h->split) {
             StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0, 0, slots != nullptr);
             p.diff = diff;
-            if (h->stamp_buf && !diff) {  // tuning: the stamp variant writes p.diff as its stamps
+            // tuning: the stamp variant's streaming gol_stencil writes p.diff as its stamps.  ONLY
+            // that kernel: gol_step1 (K = 1) and the register kernels read a non-null p.diff as a
+            // flips board of the strip's size (round 4: a K = 1 warmup launch wrote its flips over
+            // the 32 MiB stamp buffer -- an illegal memory access)
+            if (h->stamp_buf && !diff && K > 1 && pick_reg_kernel(h, s.rows, K, slots != nullptr).kind == 0 &&
+                pick_split(h, s.rows, K) <= 1 && p.nbands * (int64_t)p.nchunks <= kStampWaves) {
                 p.diff = reinterpret_cast<uint32_t *>(h->stamp_buf);
                 h->stamp_waves = p.nbands * (int64_t)p.nchunks;
             }
@@ -1019,10 +1031,16 @@ int step_block(golhip_t h, int K, int64_t slot_gen, int64_t diff_slot = kDiffNon
             const int64_t edge_waves = pb.nbands * (int64_t)pb.nchunks;
             StencilParams pi = make_params(h, s, K, K, s.rows - K, 0, 0, edge_waves, slots != nullptr);
             pb.diff = pi.diff = diff;
-            HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, pi, slots, s.compute));
+            // the bands read rows [K, 2K) and [rows - 2K, rows - K) the previous block's INTERIOR
+            // wrote: with the early exchange the halo event no longer implies it (ev_ready marks
+            // the compute stream at the end of the previous block).  Submitted before the
+            // interior: when the halos are already in place both become ready together, and the
+            // bands' few workgroups (high-priority stream) go first
+            HIPCHK(h, hipStreamWaitEvent(s.edge, s.ev_ready, 0));
             HIPCHK(h, hipStreamWaitEvent(s.edge, s.ev_halo, 0));
             HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, pb, slots, s.edge));
             HIPCHK(h, hipEventRecord(s.ev_edge, s.edge));
+            HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, pi, slots, s.compute));
             HIPCHK(h, hipStreamWaitEvent(s.compute, s.ev_edge, 0));
             h->edge_k = K;
         } else {
@@ -1091,8 +1109,7 @@ int reduce_u64(golhip_t h, const std::vector<unsigned long long *> &bufs, size_t
     if (rccl_waits(h)) {
         Shard &s = h->shards[0];
         if (h->comm_failed)
-            return fail(h, GOLHIP_ERR_RCCL, "the communicator was aborted by an earlier failure: %s",
-                        h->comm_pending.c_str());
+            return fail(h, GOLHIP_ERR_RCCL, "the communicator failed earlier: %s", h->comm_pending.c_str());
         HIPCHK(h, hipSetDevice(s.device));
         char desc[128];
         std::snprintf(desc, sizeof desc, "ncclAllReduce of %zu uint64 counts (%zu bytes) over %d ranks",
@@ -1233,8 +1250,6 @@ int transfer_bytes(golhip_t h, uint8_t *host, size_t row_stride, bool to_device)
     }
     return GOLHIP_OK;
 }
-
-constexpr int64_t kStampWaves = 1 << 20;
 
 int create_common(golhip_t h) {
     if (h->variant == golhip::kVariantStamp) {
@@ -1467,9 +1482,9 @@ int golhip_create_rank(int width, int height, int rank, int world_size, int devi
     h->rank_mode = true;
     // Test hook: GOLHIP_RING_SELF=1 makes a world-1 rank engine a ring of ONE halo'd strip whose
     // halos go through RCCL send/recv to itself, so the whole rank-mode path (plan, RCCL group,
-    // interior/boundary overlap, count all-reduce) runs on a one-GPU box.  GOLHIP_RING_SELF=2 / 3:
-    // the same ring with an unmatched receive / a comm stream stalled behind a host function, for
-    // the fail-fast tests (tests/test_gpu_failfast.py).
+    // interior/boundary overlap, count all-reduce) runs on a one-GPU box.  GOLHIP_RING_SELF=2: the
+    // same ring whose every step ends in a 20 s stall of its compute stream, for the fail-fast test
+    // of the deadline (tests/test_gpu_failfast.py).
     if (ring_self) {
         h->split = true;
         h->halo = k;
@@ -1508,13 +1523,14 @@ int golhip_create_rank(int width, int height, int rank, int world_size, int devi
         }
         if ((rc = comm_ready(h, s.comm_nccl, "the communicator's set-up (waiting for every rank)")))
             goto fail;
+        h->comm_setup_done = true;
         h->comm_pending.clear();
     }
     *out = h;
     return GOLHIP_OK;
 fail:
     g_create_error = h->err.empty() ? golhip_strerror(rc) : h->err;
-    for (auto &sh : h->shards) free_shard(sh, h->comm_timeout_ms);
+    for (auto &sh : h->shards) free_shard(sh, h->comm_timeout_ms, h->comm_failed && h->comm_setup_done);
     delete h;
     return rc;
 }
@@ -1572,7 +1588,7 @@ int golhip_destroy(golhip_t h) {
         (void)hipEventDestroy(tp.a);
         (void)hipEventDestroy(tp.b);
     }
-    for (auto &s : h->shards) free_shard(s, rccl_waits(h) ? h->comm_timeout_ms : 0);
+    for (auto &s : h->shards) free_shard(s, rccl_waits(h) ? h->comm_timeout_ms : 0, h->comm_failed);
     for (void *b : h->hc_buf)
         if (b) (void)hipHostFree(b);
     if (h->stamp_buf) (void)hipFree(h->stamp_buf);
@@ -1789,6 +1805,10 @@ static int run_steps(golhip_t h, int64_t turns, uint64_t *alive_per_turn, bool r
         int rc = flush_counts_window(h, (int)win, done - win);
         if (rc) return rc;
     }
+    if (h->test_ring_mode == 2 && rccl_waits(h))  // test hook (GOLHIP_RING_SELF=2): a stalled rank
+        HIPCHK(h, hipLaunchHostFunc(h->shards[0].compute,
+                                    [](void *) { std::this_thread::sleep_for(std::chrono::seconds(20)); },
+                                    nullptr));
     if (stop) {
         HIPCHK(h, hipSetDevice(h->shards[0].device));
         HIPCHK(h, hipEventRecord(stop, h->shards[0].compute));

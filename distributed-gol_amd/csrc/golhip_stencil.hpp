@@ -782,7 +782,7 @@ void gol_stencil(const uint32_t *__restrict__ in,
         const uint64_t t1 = __builtin_amdgcn_s_memrealtime(), c1 = __builtin_amdgcn_s_memtime();
         const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
         const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
-        if (lane == 0) {
+        if (lane == 0 && p.diff != nullptr) {  // no buffer (split boards, graphs): no stamps
             uint64_t *st = reinterpret_cast<uint64_t *>(p.diff) + 4 * wave;
             st[0] = stamp_t0;
             st[1] = t1;

@@ -508,3 +508,28 @@ def test_store_interleaved_with_steps(golhip, oracle, monkeypatch, tmp_path, sta
         e.step(3)
         ref, _ = oracle.packed_run(ref, 3)
         assert np.array_equal(e.store(), ref)
+
+
+@pytest.mark.parametrize("width,height,turns", [(65536, 65536, 120), (262144, 32768, 48), (16384, 8192, 333)])
+def test_ring_of_one_equals_single_strip_at_scale(golhip, monkeypatch, width, height, turns):
+    """The rank-mode halo path (ring of one: the early exchange, the boundary bands on the edge
+    stream, the interior on the compute stream) against the single wrapped strip on the bench's own
+    strip shapes -- where the interior launch takes hundreds of us, so a missing dependency of the
+    boundary bands on the previous interior shows (round 4: the early exchange alone let the bands
+    read rows the interior had not written yet; the 1000-turn ring of one diverged).  The single
+    strip is pinned to the oracle by the configs tests."""
+    res = {}
+    for ring in (False, True):
+        if ring:
+            monkeypatch.setenv("GOLHIP_RING_SELF", "1")
+        else:
+            monkeypatch.delenv("GOLHIP_RING_SELF", raising=False)
+        with golhip.Engine(width, height, k=16, rank=0, world_size=1, device=0) as e:
+            assert e.info.halo_rows == (16 if ring else 0)
+            e.init_random(3)
+            counts = e.step(turns, counts=True)
+            e.step(7)  # uncounted launches too (the planner's other kernels)
+            res[ring] = (counts.copy(), e.store_words())
+    monkeypatch.delenv("GOLHIP_RING_SELF", raising=False)
+    assert np.array_equal(res[True][0], res[False][0])
+    assert np.array_equal(res[True][1], res[False][1])
