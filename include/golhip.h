@@ -97,8 +97,9 @@ int golhip_create_strips(int width, int height, int nstrips, int ndevices, int k
  * GOLHIP_NCCL_ID_BYTES produced by golhip_nccl_unique_id() on rank 0 (NULL if world_size == 1).
  * Test hook: with world_size == 1 and the environment variable GOLHIP_RING_SELF=1 the board is a
  * ring of ONE halo'd strip whose halos go through RCCL send/recv to itself (the rank-mode path
- * on a single GPU); GOLHIP_RING_SELF=2 is the same ring with a top-halo receive one row longer
- * than its send (an exchange that cannot complete: the fail-fast test of golhip_set_comm_timeout).
+ * on a single GPU); GOLHIP_RING_SELF=2 is the same ring with every golhip_step ending in a 20 s
+ * stall of the compute stream (a rank whose work does not finish: the fail-fast test of
+ * golhip_set_comm_timeout).
  * The communicator is non-blocking: a rank whose peers never join fails after the comm timeout.
  * GOLHIP_RING_SELF and GOLHIP_STAGE_BYTES (the transfer stage's size in bytes, read at create;
  * tests shrink it to force many row chunks) are the only environment variables the production
@@ -241,9 +242,11 @@ int golhip_set_count_window(golhip_t h, int generations);
 /* Deadline (ms) of every host wait on work behind an RCCL transfer in rank mode -- the
  * communicator's set-up at create, a halo exchange, the count all-reduce, a sync -- plus 10x the
  * modelled time of the stencil work queued since the last sync.  When it passes (or RCCL reports an
- * asynchronous error) the communicator is aborted and the call returns GOLHIP_ERR_RCCL, with
- * golhip_last_error naming the rank, the pending operation, its peers, K and its byte count; the
- * handle then only accepts golhip_destroy.  h == NULL sets the default of later creates (120000).
+ * asynchronous error) the call returns GOLHIP_ERR_RCCL, with golhip_last_error naming the rank,
+ * the pending operation, its peers, K and its byte count; the handle then only accepts
+ * golhip_destroy.  A communicator whose set-up failed is aborted (nothing of it is on the device);
+ * after set-up it is left in place -- RCCL kernels may still be queued behind the stalled work and
+ * an abort would free state they use -- and the caller should end the process (bench.py: _exit).  h == NULL sets the default of later creates (120000).
  * The reference has no such bound: a dead server stalls Broker.Publish (broker/broker.go:58-84). */
 int golhip_set_comm_timeout(golhip_t h, int64_t ms);
 int golhip_sync(golhip_t h);                         /* wait for all queued device work */

@@ -86,7 +86,7 @@ def test_stalled_rank_fails_at_the_deadline(golhip):
     returns ERR_RCCL at the deadline -- not after the stall -- naming the last exchange; the handle
     refuses further work; destroy does not wait for the stalled stream.  Nothing RCCL is queued
     behind the stall, and the communicator is not aborted after its set-up (an abort with RCCL
-    work queued behind a stall faulted the GPU: profiles/r04/failfast.txt)."""
+    work queued behind a stall faulted the GPU: profiles/r04/r04d_failfast_abort_hooks.log)."""
     timeout_ms = 3000
     out = run_child("stall", timeout_ms, ring_self="2")
     print(json.dumps(out))
