@@ -60,6 +60,28 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "distributed-gol_amd"))
 
+
+def _hw_queues(argv) -> int:
+    """--hw-queues N (default 8; 0 leaves the environment alone), read before anything starts
+    the HIP runtime: it reads GPU_MAX_HW_QUEUES once, at its initialisation."""
+    for i, x in enumerate(argv):
+        if x == "--hw-queues" and i + 1 < len(argv):
+            return int(argv[i + 1])
+        if x.startswith("--hw-queues="):
+            return int(x.split("=", 1)[1])
+    return 8
+
+
+# HIP gives a process GPU_MAX_HW_QUEUES hardware queues (4 on the box) and maps further streams
+# onto them, serialising whatever shares one.  A rank at N > 1 runs the null stream, torch's
+# process-group streams, two RCCL communicators' internal streams and the engine's compute /
+# comm / edge streams: with 4 queues the boundary bands can land behind the interior and the
+# split step loses its overlap (the ring of one in a process holding two engines: 41-42 ms per
+# 1000 turns at 4 queues, 35.4 at 8 -- profiles/r04/r04j_hw_queues.log).
+_HWQ = _hw_queues(sys.argv[1:])
+if _HWQ > 0:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(max(_HWQ, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
+
 import torch  # noqa: E402  (first: one HIP runtime per process, see golhip.py)
 import torch.distributed as dist  # noqa: E402
 
@@ -111,6 +133,13 @@ def parse():
     ap.add_argument("--fixed-k", action="store_true",
                     help="every bulk launch exactly --k deep (PMC passes at one depth; the planner "
                          "otherwise runs its fastest measured depth <= k)")
+    ap.add_argument("--hw-queues", type=int, default=8,
+                    help="GPU_MAX_HW_QUEUES for this process (read before the HIP runtime starts; 0: "
+                         "leave the environment's)")
+    ap.add_argument("--pg-always", action="store_true",
+                    help="rehearsal of a rank's process at N > 1 on one GPU: create the torch process "
+                         "group (nccl, world 1) at N = 1 too; with GOLHIP_RING_SELF=1 the engine is the "
+                         "RCCL ring of one, so the run has every stream and communicator a rank has")
     ap.add_argument("--pg-timeout-s", type=float, default=120.0,
                     help="torch.distributed process-group timeout at N > 1 (well under a driver's "
                          "600 s bench limit: a stuck collective fails the run instead of hanging it)")
@@ -136,7 +165,7 @@ def barrier():
 
 
 def timed_steps(eng: golhip.Engine, steps: int, world: int) -> float:
-    if world > 1:
+    if dist.is_initialized():  # N > 1, or the --pg-always rehearsal
         barrier()
     torch.cuda.synchronize()
     eng.sync()
@@ -147,11 +176,11 @@ def timed_steps(eng: golhip.Engine, steps: int, world: int) -> float:
     # the engine's HIP-event span, profiles/r02/r02am_timed_region_host.txt); a golhip_sync of the
     # three engine streams before it only added ~10 us of host round trips to a 20-turn region
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         barrier()
     dt = time.perf_counter() - t0
     eng.sync()
-    if world > 1:
+    if dist.is_initialized():
         t = torch.tensor([dt], dtype=torch.float64,
                          device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -484,13 +513,19 @@ def main():
     if host_comm:
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
-    if world > 1:
+    if world > 1 or a.pg_always:
         # one process per GPU: the bench's own collectives (barriers, the max-over-ranks time, the
         # RCCL id broadcast) over RCCL; gloo where RCCL cannot run (the host-transport hook's
         # ranks share one GPU; CPU-only test runs)
         backend = "nccl" if torch.cuda.is_available() and not host_comm else "gloo"
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
         dist.init_process_group(backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=a.pg_timeout_s))
+        if world == 1:
+            obj = [None]
+            dist.broadcast_object_list(obj, src=0)  # the collective N > 1 runs before the engine
     golhip.set_default_comm_timeout(a.comm_timeout_ms)
 
     width = a.size
@@ -805,7 +840,10 @@ def main():
             "untimed_generations_before_value": (
                 a.warmup + (a.warmup + a.steps + cold["preheat_turns"] if cold else 0)),
             "transport": "gloo host transport (test hook GOLHIP_HOST_COMM=1)" if host_comm else
-                         ("rccl" if world > 1 else None),
+                         ("rccl" if world > 1 else
+                          "rccl ring of one (GOLHIP_RING_SELF=1)" if os.environ.get("GOLHIP_RING_SELF") == "1" else None),
+            "process": {"gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+                        "process_group": dist.get_backend() if dist.is_initialized() else None},
             # the same warmup + timed turns measured first, on the chip as the process found it
             # (idle clock): what a 20-turn run pays before the clock has ramped
             "cold_start": cold,
@@ -831,7 +869,7 @@ def main():
             "alive_after": int(checksum),
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
     # a wrong board is not a result: the line above is printed for the record, then the run fails
     bad = ((parity and not parity["ok"]) or (strong and strong.get("parity") and not strong["parity"]["ok"])

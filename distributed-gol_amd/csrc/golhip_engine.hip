@@ -122,9 +122,14 @@ struct golhip_engine {
     int force_split = 0;  // 0 = automatic
     int force_tile = -1;  // -1 automatic, 0 never, T > 0 always (tile height T)
     int force_slab = -1;  // -1 automatic, 0 never, [NC*10000 +] W*100 + S always (slab shape)
+    bool edge_prio = false;   // tuning: comm/edge streams at high priority (GOLHIP_EDGE_PRIO)
+    bool edge_first = false;  // tuning: boundary bands submitted before the interior
+    // the boundary bands' waves raise their issue priority (StencilParams::prio); tuning knob
+    // GOLHIP_EDGE_SETPRIO=0 turns it off for A/B
+    int edge_setprio = 1;
     int graph_mode = -1;  // golhip_set_graphs: -1 automatic, 0 never, 1 whenever the plan allows
     // RCCL fail-fast (rank mode): every host wait on work that can depend on an RCCL transfer polls
-    // ncclCommGetAsyncError against a deadline and aborts the communicator when it passes
+    // ncclCommGetAsyncError against a deadline and fails the handle when it passes
     // (golhip_set_comm_timeout); the communicator is non-blocking, so no RCCL call blocks the host
     int64_t comm_timeout_ms = 0;
     double queued_s = 0.0;  // modelled seconds of stencil work queued since the last full sync
@@ -346,13 +351,14 @@ constexpr int64_t kStageBytes = 64ll << 20;
 int alloc_shard(golhip_t h, Shard &s) {
     HIPCHK(h, hipSetDevice(s.device));
     HIPCHK(h, hipStreamCreateWithFlags(&s.compute, hipStreamNonBlocking));
-    // the halo exchange and the boundary bands are short and on the critical path of a split
-    // board's block (the next exchange waits for the bands): their streams get the device's highest
-    // priority, so their few workgroups are dispatched ahead of the interior's waiting ones
+    // comm and edge streams at the default priority: high-priority queues for them (so the bands'
+    // few workgroups dispatch ahead of the interior's) ran the 65536^2 ring of one 16 % SLOWER over
+    // 1000 turns (r04g vs r04f, profiles/r04/r04h_edge_ab_p*.log); kept as a tuning knob
     int lo_prio = 0, hi_prio = 0;
     HIPCHK(h, hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
-    HIPCHK(h, hipStreamCreateWithPriority(&s.comm, hipStreamNonBlocking, hi_prio));
-    HIPCHK(h, hipStreamCreateWithPriority(&s.edge, hipStreamNonBlocking, hi_prio));
+    const int edge_prio = h->edge_prio ? hi_prio : lo_prio;
+    HIPCHK(h, hipStreamCreateWithPriority(&s.comm, hipStreamNonBlocking, edge_prio));
+    HIPCHK(h, hipStreamCreateWithPriority(&s.edge, hipStreamNonBlocking, edge_prio));
     HIPCHK(h, hipEventCreateWithFlags(&s.ev_ready, hipEventDisableTiming));
     HIPCHK(h, hipEventCreateWithFlags(&s.ev_halo, hipEventDisableTiming));
     HIPCHK(h, hipEventCreateWithFlags(&s.ev_edge, hipEventDisableTiming));
@@ -471,6 +477,9 @@ int setup_engine(golhip_t h, int width, int height, int world, int k) {
     if (const char *e = std::getenv("GOLHIP_SPLIT")) h->force_split = std::atoi(e);
     if (const char *e = std::getenv("GOLHIP_TILE")) h->force_tile = std::atoi(e);
     if (const char *e = std::getenv("GOLHIP_SLAB")) h->force_slab = std::atoi(e);
+    if (const char *e = std::getenv("GOLHIP_EDGE_PRIO")) h->edge_prio = std::atoi(e) != 0;
+    if (const char *e = std::getenv("GOLHIP_EDGE_FIRST")) h->edge_first = std::atoi(e) != 0;
+    if (const char *e = std::getenv("GOLHIP_EDGE_SETPRIO")) h->edge_setprio = std::atoi(e) != 0;
     if (const char *e = std::getenv("GOLHIP_VARIANT"))
         h->variant = std::strcmp(e, "chain") == 0     ? golhip::kVariantChain
                      : std::strcmp(e, "skew") == 0   ? golhip::kVariantSkew
@@ -1031,16 +1040,19 @@ int step_block(golhip_t h, int K, int64_t slot_gen, int64_t diff_slot = kDiffNon
             const int64_t edge_waves = pb.nbands * (int64_t)pb.nchunks;
             StencilParams pi = make_params(h, s, K, K, s.rows - K, 0, 0, edge_waves, slots != nullptr);
             pb.diff = pi.diff = diff;
+            pb.prio = h->edge_setprio;
             // the bands read rows [K, 2K) and [rows - 2K, rows - K) the previous block's INTERIOR
             // wrote: with the early exchange the halo event no longer implies it (ev_ready marks
-            // the compute stream at the end of the previous block).  Submitted before the
-            // interior: when the halos are already in place both become ready together, and the
-            // bands' few workgroups (high-priority stream) go first
+            // the compute stream at the end of the previous block).  Submission order (interior
+            // first by default; edge_first: tuning A/B) only matters when both are ready at once
+            if (!h->edge_first)
+                HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, pi, slots, s.compute));
             HIPCHK(h, hipStreamWaitEvent(s.edge, s.ev_ready, 0));
             HIPCHK(h, hipStreamWaitEvent(s.edge, s.ev_halo, 0));
             HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, pb, slots, s.edge));
             HIPCHK(h, hipEventRecord(s.ev_edge, s.edge));
-            HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, pi, slots, s.compute));
+            if (h->edge_first)
+                HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, pi, slots, s.compute));
             HIPCHK(h, hipStreamWaitEvent(s.compute, s.ev_edge, 0));
             h->edge_k = K;
         } else {

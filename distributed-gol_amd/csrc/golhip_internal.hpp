@@ -46,6 +46,9 @@ struct StencilParams {
     int64_t lo, hi;      // halo mode: readable input rows [lo, hi) relative to row 0
     int32_t wd;          // words per row of the torus
     int32_t nchunks;     // column chunks per row (chunk_words() words each)
+    // 1: the waves raise their issue priority (s_setprio 3) -- the split step's boundary bands,
+    // a few dozen waves on the critical path that share SIMDs with the interior's (gol_stencil)
+    int32_t prio;
     // nullable: row 0 of a board (same pitch and rows) that receives the XOR of the output
     // generation with the one before it -- the cells the launch's last generation flipped
     // (gol/distributor.go:53-59), written beside the output rows (no extra pass)

@@ -411,6 +411,9 @@ void gol_stencil(const uint32_t *__restrict__ in,
     const int64_t chunk = wave % p.nchunks;
     const int64_t bandi = wave / p.nchunks;
     if (bandi >= p.nbands) return;  // wave-uniform
+    // the split step's boundary bands (p.prio, uniform): issue ahead of the interior's waves on
+    // the same SIMD, so the chain bands -> halo exchange -> next bands is not starved
+    if (p.prio) __builtin_amdgcn_s_setprio(3);
     uint64_t stamp_t0 = 0, stamp_c0 = 0;
     if constexpr (STAMP) {
         stamp_t0 = __builtin_amdgcn_s_memrealtime();

@@ -17,7 +17,7 @@ exchange is shorter than it, and the end-of-region barrier).
 
 Each shape: one single-strip and one ring-of-one engine on the same seeded board, pre-heated,
 alternating rounds; the alive counts of both must agree.
-Usage: predict_scaling.py [rounds] [weak turns list] [strong turns]"""
+Usage: predict_scaling.py [rounds] [weak turns list] [strong turns] [strong gpus list]"""
 import json
 import os
 import statistics
@@ -34,6 +34,8 @@ import golhip  # noqa: E402
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 weak_turns = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "20,1000").split(",")]
 strong_turns = int(sys.argv[3]) if len(sys.argv) > 3 else 160
+strong_gpus = [int(x) for x in (sys.argv[4] if len(sys.argv) > 4 else "1,2,4,8").split(",")]
+assert strong_gpus[0] == 1
 K = 16
 
 
@@ -95,7 +97,7 @@ for turns in weak_turns:
     out["weak"].append(m)
     print(json.dumps(m), flush=True)
 base = None
-for G in (1, 2, 4, 8):
+for G in (strong_gpus if strong_turns > 0 else []):
     rows = 262144 // G
     m = measure(262144, rows, 4, K, strong_turns)
     if G == 1:
