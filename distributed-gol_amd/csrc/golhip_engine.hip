@@ -146,6 +146,7 @@ struct golhip_engine {
     // tuning build, GOLHIP_VARIANT=stamp: per-wave timestamps of the last single-strip launch
     uint64_t *stamp_buf = nullptr;
     int64_t stamp_waves = 0;
+    int stamp_words = 4;  // uint64 per wave of the last stamped launch (gol_slab2: 8)
     std::vector<Shard> shards;
     int cur = 0;
     bool prev_valid = false;
@@ -1026,6 +1027,16 @@ int step_block(golhip_t h, int K, int64_t slot_gen, int64_t diff_slot = kDiffNon
                 pick_split(h, s.rows, K) <= 1 && p.nbands * (int64_t)p.nchunks <= kStampWaves) {
                 p.diff = reinterpret_cast<uint32_t *>(h->stamp_buf);
                 h->stamp_waves = p.nbands * (int64_t)p.nchunks;
+                h->stamp_words = 4;
+            } else if (h->stamp_buf && !diff && K > 1) {
+                // gol_slab2 writes its phase stamps through p.stamp (never p.diff)
+                const RegKernel rk = pick_reg_kernel(h, s.rows, K, slots != nullptr);
+                if (rk.kind == 3 && (rk.NC == 9 || rk.NC == 10) /* gol_slab2 / gol_slab3 */ &&
+                    8 * p.nbands * (int64_t)p.nchunks * rk.W <= 4 * kStampWaves) {
+                    p.stamp = h->stamp_buf;
+                    h->stamp_waves = p.nbands * (int64_t)p.nchunks * rk.W;
+                    h->stamp_words = 8;
+                }
             }
             // a K-deep ring launch (ring_depth: a production register slab) writes the flips of
             // each of its K generations into K consecutive ring slots
@@ -1621,6 +1632,21 @@ int golhip_tuning_stamps(golhip_t h, uint64_t *out, size_t cap_waves, size_t *n_
     if (!out) return GOLHIP_OK;
     if (cap_waves < *n_waves) return GOLHIP_ERR_CAP;
     HIPCHK(h, hipMemcpy(out, h->stamp_buf, sizeof(uint64_t) * 4 * *n_waves, hipMemcpyDeviceToHost));
+    return GOLHIP_OK;
+}
+// The same with the record length: words_per_wave uint64 per wave (4: gol_stencil, 8: gol_slab2's
+// phase stamps -- start, rows loaded, generations done, end, cycles, HW_ID | XCC_ID << 32, group,
+// wave).  cap_words / n_words count uint64.  scripts/slab_stamps.py.
+int golhip_tuning_stamps_ex(golhip_t h, uint64_t *out, size_t cap_words, size_t *n_words, int *words_per_wave) {
+    if (!h || !n_words || !words_per_wave) return GOLHIP_ERR_ARG;
+    if (!h->stamp_buf) return fail(h, GOLHIP_ERR_STATE, "not a GOLHIP_VARIANT=stamp handle");
+    int rc = sync_all(h);
+    if (rc) return rc;
+    *words_per_wave = h->stamp_words;
+    *n_words = (size_t)std::min<int64_t>(h->stamp_waves * h->stamp_words, 4 * kStampWaves);
+    if (!out) return GOLHIP_OK;
+    if (cap_words < *n_words) return GOLHIP_ERR_CAP;
+    HIPCHK(h, hipMemcpy(out, h->stamp_buf, sizeof(uint64_t) * *n_words, hipMemcpyDeviceToHost));
     return GOLHIP_OK;
 }
 #endif

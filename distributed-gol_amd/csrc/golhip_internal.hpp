@@ -56,6 +56,9 @@ struct StencilParams {
     // > 0 (gol_slab only; golhip_step_flips): EVERY generation g (0-based) of the launch writes its
     // flips to diff + g * diff_stride words (consecutive slots of the per-turn flips ring)
     int64_t diff_stride;
+    // tuning build only (null otherwise): gol_slab2's per-wave phase stamps, 8 uint64 per wave
+    // (golhip_tuning_stamps_ex, scripts/slab_stamps.py)
+    uint64_t *stamp;
 };
 
 constexpr int kMaxK = 32;         // generations per launch limit (halo lane = 32 bits)

@@ -606,6 +606,11 @@ __global__ __launch_bounds__(64 * W) void gol_slab2(const uint32_t *__restrict__
     const int64_t per_xcd = (ngroups + kXcds - 1) / kXcds;
     const int64_t group = (int64_t)(blockIdx.x % kXcds) * per_xcd + blockIdx.x / kXcds;
     if (group >= ngroups) return;  // whole workgroup
+    // tuning build, p.stamp: phase stamps of every wave (start, rows loaded, generations done, end;
+    // s_memrealtime 100 MHz), its shader cycles and HW_ID / XCC_ID
+    uint64_t st_t0 = 0, st_c0 = 0, st_t1 = 0, st_t2 = 0;
+    if constexpr (kTuningBuild)
+        if (p.stamp) st_t0 = __builtin_amdgcn_s_memrealtime(), st_c0 = __builtin_amdgcn_s_memtime();
     const int64_t chunk = group % p.nchunks;
     const int64_t bandi = group / p.nchunks;
     int ya, yb;
@@ -617,6 +622,11 @@ __global__ __launch_bounds__(64 * W) void gol_slab2(const uint32_t *__restrict__
     uint32_t c[S + 2];  // rows 1..S of this wave (c[0], c[S + 1] unused)
     c[0] = c[S + 1] = 0;
     load_rows<1, S>(c, in, p, ya - K + w * S, col);
+    if constexpr (kTuningBuild)
+        if (p.stamp) {
+            __builtin_amdgcn_s_waitcnt(0);  // the rows are in (stamp runs only)
+            st_t1 = __builtin_amdgcn_s_memrealtime();
+        }
     const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
         out + (int64_t)ya * p.pitch, 0, nrows * rowbytes, kBufferRsrcWord3);
     __amdgpu_buffer_rsrc_t drsrc = orsrc;
@@ -767,6 +777,8 @@ __global__ __launch_bounds__(64 * W) void gol_slab2(const uint32_t *__restrict__
         for (int g = 1; g < K; ++g) gen(No{}, No{}, Yes{}, g);
         gen(Yes{}, No{}, Yes{}, K);
     }
+    if constexpr (kTuningBuild)
+        if (p.stamp) st_t2 = __builtin_amdgcn_s_memrealtime();
     if constexpr (COUNT) {  // the generations not flushed yet
         lds_barrier();
         if constexpr (2 * S <= K) {
@@ -781,6 +793,273 @@ __global__ __launch_bounds__(64 * W) void gol_slab2(const uint32_t *__restrict__
             }
         }
     }
+    if constexpr (kTuningBuild)
+        if (p.stamp) {
+            __builtin_amdgcn_s_waitcnt(0);  // the stores and count atomics have left the wave
+            const uint64_t t3 = __builtin_amdgcn_s_memrealtime(), c1 = __builtin_amdgcn_s_memtime();
+            const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+            const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+            if (lane == 0) {
+                uint64_t *r = p.stamp + 8 * (group * W + w);
+                r[0] = st_t0, r[1] = st_t1, r[2] = st_t2, r[3] = t3;
+                r[4] = c1 - st_c0, r[5] = (uint64_t)hw | ((uint64_t)xcc << 32);
+                r[6] = (uint64_t)group, r[7] = (uint64_t)w;
+            }
+        }
+}
+
+// gol_slab3: gol_slab2 software-pipelined across generations.  The phase stamps of gol_slab2
+// (profiles/r04/r04n_slab_stamps.log: configs[1] 5120^2 with every count, 14.4 us per 16-turn
+// launch, 10.5 of them in the generation loop, 0.66 us per generation for ~0.4 us of VALU issue)
+// put the loss inside the loop: after each generation's barrier a wave reads its neighbours' edge
+// sums from LDS and must wait for them, then updates only its two edge rows -- two dependency
+// chains per wave, two waves per SIMD.  Here the work after the barrier starts with independent
+// rows: iteration g (after barrier g) issues the LDS reads of the neighbours' sums of generation
+// g - 1, computes the sums of the S - 2 interior rows of generation g (which were finished before
+// the barrier) while the reads are in flight, then the two edge rows of generation g, their sums
+// and their publication for barrier g + 1, and the interior rows of generation g + 1.  The same
+// instructions as gol_slab2 in another order; the LDS round trip and the short edge chains overlap
+// S - 2 rows of independent work.
+template <int K, int W, int S, bool COUNT, int LD>
+__global__ __launch_bounds__(64 * W) void gol_slab3(const uint32_t *__restrict__ in,
+                                                    uint32_t *__restrict__ out, StencilParams p,
+                                                    unsigned long long *__restrict__ slots) {
+    constexpr int T = W * S - 2 * K;
+    static_assert(T >= 1 && K >= 3 && K <= 32 && W >= 2 && S >= 4, "slab geometry");
+    __shared__ uint32_t ex[2][W + 2][4][64];  // as gol_slab: wave w's block is ex[par][w + 1]
+    __shared__ uint32_t cnt_lds[COUNT ? K : 1][COUNT ? W : 1][64];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int64_t ngroups = p.nbands * (int64_t)p.nchunks;
+    const int64_t per_xcd = (ngroups + kXcds - 1) / kXcds;
+    const int64_t group = (int64_t)(blockIdx.x % kXcds) * per_xcd + blockIdx.x / kXcds;
+    if (group >= ngroups) return;  // whole workgroup
+    uint64_t st_t0 = 0, st_c0 = 0, st_t1 = 0, st_t2 = 0;
+    if constexpr (kTuningBuild)
+        if (p.stamp) st_t0 = __builtin_amdgcn_s_memrealtime(), st_c0 = __builtin_amdgcn_s_memtime();
+    const int64_t chunk = group % p.nchunks;
+    const int64_t bandi = group / p.nchunks;
+    int ya, yb;
+    band_rows(p, bandi, ya, yb);
+    const int nrows = yb - ya;
+    const int colraw = (int)chunk * kTileChunkWords + lane - 1;
+    const int col = (colraw + p.wd) % p.wd;
+    const int rowbytes = (int)(p.pitch * 4);
+    uint32_t c[S + 2];  // rows 1..S of this wave (c[0], c[S + 1] unused)
+    c[0] = c[S + 1] = 0;
+    load_rows<1, S>(c, in, p, ya - K + w * S, col);
+    if constexpr (kTuningBuild)
+        if (p.stamp) {
+            __builtin_amdgcn_s_waitcnt(0);
+            st_t1 = __builtin_amdgcn_s_memrealtime();
+        }
+    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+        out + (int64_t)ya * p.pitch, 0, nrows * rowbytes, kBufferRsrcWord3);
+    __amdgpu_buffer_rsrc_t drsrc = orsrc;
+    if constexpr (LD == 1)
+        drsrc = __builtin_amdgcn_make_buffer_rsrc(p.diff + (int64_t)ya * p.pitch, 0,
+                                                  nrows * rowbytes, kBufferRsrcWord3);
+    const LaneStore ls = lane_store<false>(lane, colraw, col, p.wd);
+    const bool count_lane = lane >= 2 && colraw <= p.wd;
+    const int o0 = w * S - K;  // output row of c[1]
+    if constexpr (COUNT)
+        for (int j = 0; j < K; ++j) cnt_lds[j][w][lane] = 0;
+    if (w == 0)
+        for (int par = 0; par < 2; ++par)
+            for (int i = 0; i < 4; ++i) ex[par][0][i][lane] = ex[par][W + 1][i][lane] = 0u;
+    uint32_t *const ex_base0 = &ex[0][w][0][lane];
+    constexpr int kExPar = (W + 2) * 4 * 64;
+    uint32_t *const cnt_my = &cnt_lds[0][w][lane];
+    auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    auto cnt_sum = [&](int j) {
+        uint32_t a = 0;
+#pragma unroll
+        for (int ww = 0; ww < W; ++ww) a += cnt_lds[j][ww][lane];
+        return count_lane ? a : 0u;
+    };
+    auto flush_after_barrier = [&](int g) {
+        if constexpr (COUNT && 2 * S <= K) {
+            if (g >= 2 && w == ((g & 1) ? W - 1 : 0)) {
+                uint32_t acc[1] = {cnt_sum(g - 2)};
+                flush_counts<1>(acc, g - 2, lane, group, slots);
+            }
+        }
+    };
+    const bool full = o0 >= 0 && o0 + S <= nrows;
+    const bool halo = o0 + S <= 0 || o0 >= nrows;
+    // the sums (s, cy) and drifted centres (ctr) of the wave's S rows of the last generation whose
+    // rows are complete; cnt: the popcount of the generation being assembled
+    uint32_t s[S], cy[S], ctr[S];
+    uint32_t cnt = 0;
+    // row r (1..S) of generation gi (0-based): counts, flips, the output store of the last one
+    auto emit = [&](auto last_c, auto full_c, auto cnt_c, int r, uint32_t nx, uint32_t centre, int gi) {
+        constexpr bool LAST = decltype(last_c)::value, FULL = decltype(full_c)::value;
+        constexpr bool CNT = COUNT && decltype(cnt_c)::value;
+        const int o = o0 + r - 1;
+        const bool mine = FULL || (o >= 0 && o < nrows);  // wave-uniform
+        if (CNT) cnt = bcnt_acc(mine ? nx : 0u, cnt);
+        if constexpr (LD == 2) {
+            const __amdgpu_buffer_rsrc_t grsrc = __builtin_amdgcn_make_buffer_rsrc(
+                p.diff + gi * p.diff_stride + (int64_t)ya * p.pitch, 0, nrows * rowbytes, kBufferRsrcWord3);
+            Words<1> dv;
+            dv.w[0] = realign_drift_rt(nx ^ centre, gi);
+            golhip::store_row<1, false>(grsrc, ls, dv, mine ? o * rowbytes : kOutOfRange);
+        }
+        if constexpr (LAST) {
+            const int rowoff = mine ? o * rowbytes : kOutOfRange;
+            Words<1> v;
+            v.w[0] = realign_drift<K>(nx);
+            golhip::store_row<1, false>(orsrc, ls, v, rowoff);
+            if constexpr (LD == 1) {
+                Words<1> dv;
+                dv.w[0] = realign_drift<K>(nx ^ centre);
+                golhip::store_row<1, false>(drsrc, ls, dv, rowoff);
+            }
+        }
+    };
+    auto publish = [&](int g) {  // the edge rows' sums read by the neighbours after barrier g
+        uint32_t *const b = ex_base0 + (g & 1) * kExPar;
+        b[256] = s[0];
+        b[320] = cy[0];
+        b[384] = s[S - 1];
+        b[448] = cy[S - 1];
+    };
+    // the interior rows 2..S-1 of generation gi (0-based) from the sums of all S rows
+    auto interior = [&](auto last_c, auto full_c, auto cnt_c, int gi) {
+        constexpr int NI = S - 2;
+        uint32_t as[NI], acy[NI], ms[NI], mcy[NI], mc[NI], bs[NI], bcy[NI], nx[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            as[i] = s[i], acy[i] = cy[i];
+            ms[i] = s[i + 1], mcy[i] = cy[i + 1], mc[i] = ctr[i + 1];
+            bs[i] = s[i + 2], bcy[i] = cy[i + 2];
+        }
+        life_om<NI>(as, acy, ms, mcy, mc, bs, bcy, nx, AllRows{});
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            emit(last_c, full_c, cnt_c, i + 2, nx[i], mc[i], gi);
+            c[i + 2] = nx[i];
+        }
+    };
+    // iteration g (1-based, after barrier g): generation g's edge rows; with NEXT, generation
+    // g + 1's interior rows (LASTI: that is the launch's last generation)
+    auto iter = [&](auto laste_c, auto next_c, auto lasti_c, auto full_c, auto cnt_c, int g) {
+        constexpr bool NEXT = decltype(next_c)::value;
+        lds_barrier();
+        const uint32_t *const b = ex_base0 + (g & 1) * kExPar;
+        const uint32_t ts = b[128], tcy = b[192];    // the upper neighbour's last row
+        const uint32_t bts = b[512], btcy = b[576];  // the lower neighbour's first row
+        flush_after_barrier(g);
+        // generation g - 1's sums of rows 1, 2, S - 1, S and centres of 1, S
+        const uint32_t es0 = s[0], ecy0 = cy[0], ec0 = ctr[0], ns0 = s[1], ncy0 = cy[1];
+        const uint32_t es1 = s[S - 1], ecy1 = cy[S - 1], ec1 = ctr[S - 1], ns1 = s[S - 2], ncy1 = cy[S - 2];
+        if constexpr (NEXT) {  // generation g's interior rows (done before the barrier): their sums
+            uint32_t x[S - 2], s2[S - 2], cy2[S - 2], c2[S - 2];
+#pragma unroll
+            for (int i = 0; i < S - 2; ++i) x[i] = c[i + 2];
+            sums_om<S - 2>(x, s2, cy2, c2);
+#pragma unroll
+            for (int i = 0; i < S - 2; ++i) s[i + 1] = s2[i], cy[i + 1] = cy2[i], ctr[i + 1] = c2[i];
+        }
+        {  // generation g's edge rows, from the neighbours' sums
+            uint32_t as[2] = {ts, ns1}, acy[2] = {tcy, ncy1};
+            uint32_t ms[2] = {es0, es1}, mcy[2] = {ecy0, ecy1}, mc[2] = {ec0, ec1};
+            uint32_t bs[2] = {ns0, bts}, bcy[2] = {ncy0, btcy}, nx[2];
+            life_om<2>(as, acy, ms, mcy, mc, bs, bcy, nx, AllRows{});
+            emit(laste_c, full_c, cnt_c, 1, nx[0], mc[0], g - 1);
+            emit(laste_c, full_c, cnt_c, S, nx[1], mc[1], g - 1);
+            c[1] = nx[0];
+            c[S] = nx[1];
+        }
+        if constexpr (COUNT && decltype(cnt_c)::value) {
+            cnt_my[(g - 1) * (W * 64)] = cnt;
+            cnt = 0;
+        }
+        if constexpr (NEXT) {  // the edge rows' sums, published for barrier g + 1
+            uint32_t x[2] = {c[1], c[S]}, s2[2], cy2[2], c2[2];
+            sums_om<2>(x, s2, cy2, c2);
+            s[0] = s2[0], cy[0] = cy2[0], ctr[0] = c2[0];
+            s[S - 1] = s2[1], cy[S - 1] = cy2[1], ctr[S - 1] = c2[1];
+            publish(g + 1);
+            interior(lasti_c, full_c, cnt_c, g);  // generation g + 1 (0-based g)
+        }
+    };
+    using No = std::false_type;
+    using Yes = std::true_type;
+    // prologue: the sums of the loaded rows, their edge sums for barrier 1, generation 1's interior
+    {
+        uint32_t x[S];
+#pragma unroll
+        for (int i = 0; i < S; ++i) x[i] = c[i + 1];
+        sums_om<S>(x, s, cy, ctr);
+        publish(1);
+    }
+    // the full loop of a wave with output rows: generations 1 .. K
+    auto run_all = [&](auto full_c, auto cnt_c) {
+        interior(No{}, full_c, cnt_c, 0);
+#pragma clang loop unroll(disable)
+        for (int g = 1; g < K - 1; ++g) iter(No{}, Yes{}, No{}, full_c, cnt_c, g);
+        iter(No{}, Yes{}, Yes{}, full_c, cnt_c, K - 1);
+        iter(Yes{}, No{}, No{}, full_c, cnt_c, K);
+    };
+    if constexpr (LD == 2 || !COUNT) {
+        run_all(No{}, Yes{});
+    } else if (halo) {
+        // a pure-halo wave computes while its rows can still reach an output row, then only keeps
+        // the barrier count (gol_slab2's g_end; its last publication -- generation g_end - 1's edge
+        // sums, read after barrier g_end -- happens in iteration g_end - 1)
+        const int g_end = std::min(std::min(w * S + S, W * S - w * S), K);
+        interior(No{}, No{}, No{}, 0);
+        int g = 1;
+#pragma clang loop unroll(disable)
+        for (; g < g_end && g < K - 1; ++g) iter(No{}, Yes{}, No{}, No{}, No{}, g);
+        if (g < g_end && g == K - 1) {
+            iter(No{}, Yes{}, Yes{}, No{}, No{}, g);
+            ++g;
+        }
+        if (g < g_end && g == K) {
+            iter(Yes{}, No{}, No{}, No{}, No{}, g);
+            ++g;
+        }
+#pragma clang loop unroll(disable)
+        for (; g <= K; ++g) {
+            lds_barrier();
+            flush_after_barrier(g);
+        }
+    } else if (full) {
+        run_all(Yes{}, Yes{});
+    } else {
+        run_all(No{}, Yes{});
+    }
+    if constexpr (kTuningBuild)
+        if (p.stamp) st_t2 = __builtin_amdgcn_s_memrealtime();
+    if constexpr (COUNT) {  // the generations not flushed yet
+        lds_barrier();
+        if constexpr (2 * S <= K) {
+            if (w == ((K & 1) ? 0 : W - 1)) {
+                uint32_t acc[1] = {cnt_sum(K - 1)};
+                flush_counts<1>(acc, K - 1, lane, group, slots);
+            }
+        } else {
+            for (int j = w; j < K; j += W) {
+                uint32_t acc[1] = {cnt_sum(j)};
+                flush_counts<1>(acc, j, lane, group, slots);
+            }
+        }
+    }
+    if constexpr (kTuningBuild)
+        if (p.stamp) {
+            __builtin_amdgcn_s_waitcnt(0);
+            const uint64_t t3 = __builtin_amdgcn_s_memrealtime(), c1 = __builtin_amdgcn_s_memtime();
+            const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
+            const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+            if (lane == 0) {
+                uint64_t *r = p.stamp + 8 * (group * W + w);
+                r[0] = st_t0, r[1] = st_t1, r[2] = st_t2, r[3] = t3;
+                r[4] = c1 - st_c0, r[5] = (uint64_t)hw | ((uint64_t)xcc << 32);
+                r[6] = (uint64_t)group, r[7] = (uint64_t)w;
+            }
+        }
 }
 
 template <int K, int T>
@@ -804,13 +1083,14 @@ hipError_t launch_tile_kt(const uint32_t *in, uint32_t *out, const StencilParams
 // The production slab shapes (pick_reg_kernel): only these instantiate the every-generation
 // flips variant (LD = 2).  NC = kSlab2 selects gol_slab2 (the edge hand-off off the critical path).
 constexpr int kSlab2 = 9;
+constexpr int kSlab3 = 10;  // gol_slab3: gol_slab2 pipelined across generations
 constexpr bool slab_prod_ws(int K, int W, int S) {
     return (K == 16 && W == 8 && S == 12) || (K == 16 && W == 12 && S == 8) ||
            (K == 16 && W == 12 && S == 7) || (K == 16 && W == 16 && S == 6) || (K == 8 && W == 8 && S == 8) ||
            (K == 12 && W == 8 && S == 8);
 }
 constexpr bool slab_prod_shape(int K, int W, int S, int NC) {
-    return slab_prod_ws(K, W, S) && (NC == kSlab2 || (K == 16 ? NC == 2 : NC == 4));
+    return slab_prod_ws(K, W, S) && (NC == kSlab2 || NC == kSlab3 || (K == 16 ? NC == 2 : NC == 4));
 }
 
 template <int K, int W, int S, int NC>
@@ -819,6 +1099,29 @@ hipError_t launch_slab_kws(const uint32_t *in, uint32_t *out, const StencilParam
     const int64_t ngroups = p.nbands * (int64_t)p.nchunks;
     const unsigned blocks = (unsigned)std::max<int64_t>(1, (ngroups + kXcds - 1) / kXcds * kXcds);
     const dim3 block(64 * W);
+    if constexpr (NC == kSlab3) {
+        if (p.diff && p.diff_stride > 0) {
+            if constexpr (slab_prod_shape(K, W, S, NC)) {
+                if (slots)
+                    hipLaunchKernelGGL((gol_slab3<K, W, S, true, 2>), dim3(blocks), block, 0, s, in, out, p, slots);
+                else
+                    hipLaunchKernelGGL((gol_slab3<K, W, S, false, 2>), dim3(blocks), block, 0, s, in, out, p, slots);
+                return hipGetLastError();
+            } else {
+                return hipErrorNotSupported;
+            }
+        }
+        const int ld = p.diff ? 1 : 0;
+        if (ld && slots)
+            hipLaunchKernelGGL((gol_slab3<K, W, S, true, 1>), dim3(blocks), block, 0, s, in, out, p, slots);
+        else if (ld)
+            hipLaunchKernelGGL((gol_slab3<K, W, S, false, 1>), dim3(blocks), block, 0, s, in, out, p, slots);
+        else if (slots)
+            hipLaunchKernelGGL((gol_slab3<K, W, S, true, 0>), dim3(blocks), block, 0, s, in, out, p, slots);
+        else
+            hipLaunchKernelGGL((gol_slab3<K, W, S, false, 0>), dim3(blocks), block, 0, s, in, out, p, slots);
+        return hipGetLastError();
+    }
     if constexpr (NC == kSlab2) {
         if (p.diff && p.diff_stride > 0) {
             if constexpr (slab_prod_shape(K, W, S, NC)) {
@@ -880,7 +1183,8 @@ hipError_t launch_slab_kws(const uint32_t *in, uint32_t *out, const StencilParam
     X(16, 8, 12, 2) X(16, 12, 8, 2) X(16, 12, 7, 2) \
     X(8, 8, 4, 4) X(16, 8, 8, 4) X(16, 8, 12, 4) X(16, 16, 8, 4) \
     X(16, 12, 8, 4) X(16, 10, 8, 2) X(16, 14, 6, 2) X(16, 16, 6, 2) X(16, 16, 5, 2) \
-    X(8, 8, 8, 9) X(12, 8, 8, 9) X(16, 16, 5, 9) X(16, 10, 8, 9) X(16, 8, 8, 9) X(16, 12, 6, 9)
+    X(8, 8, 8, 9) X(12, 8, 8, 9) X(16, 16, 5, 9) X(16, 10, 8, 9) X(16, 8, 8, 9) X(16, 12, 6, 9) \
+    X(16, 8, 12, 10) X(16, 16, 6, 10) X(16, 12, 8, 10) X(16, 12, 7, 10) X(16, 10, 8, 10) X(16, 8, 10, 10)
 #define GOLHIP_TILE_CONFIGS(X) \
     X(2, 16) X(4, 8) X(4, 16) X(4, 32) X(6, 16) X(8, 8) X(8, 16) X(8, 32) X(10, 16) X(12, 8) \
     X(12, 16) X(12, 32) X(14, 16) X(16, 8) X(16, 16) X(16, 32)

@@ -3,7 +3,7 @@
 --kernel-trace CSV: where the boundary bands, the interior and the RCCL send/recv of each block
 run relative to each other, and what the block's wall time is made of.
 
-  run:     ring_timeline.py run [size] [turns] [ring 0/1]   (under rocprofv3 --kernel-trace)
+  run:     ring_timeline.py run [size] [turns] [ring 0/1] [warmup]   (under rocprofv3 --kernel-trace)
   analyse: ring_timeline.py <trace dir> [blocks to print] [last blocks analysed (default 70)]"""
 import csv
 import glob
@@ -26,6 +26,7 @@ if sys.argv[1] == "run":
     size = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
     turns = int(sys.argv[3]) if len(sys.argv) > 3 else 1000
     ring = sys.argv[4] != "0" if len(sys.argv) > 4 else True
+    warm = int(sys.argv[5]) if len(sys.argv) > 5 else 8
     if ring:
         os.environ["GOLHIP_RING_SELF"] = "1"
     e = golhip.Engine(size, size, k=16, rank=0, world_size=1, device=0)
@@ -35,7 +36,7 @@ if sys.argv[1] == "run":
         e.step(32)
         e.sync()
     e.init_random(3)
-    e.step(8)
+    e.step(warm)
     e.sync()
     t = time.perf_counter()
     e.step(turns)

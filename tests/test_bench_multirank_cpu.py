@@ -17,6 +17,7 @@ import json
 import os
 import socket
 import sys
+from pathlib import Path
 
 import numpy as np
 import pytest
@@ -186,6 +187,7 @@ def _worker(rank, world, port, out_dir):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_bench_rank_path_cpu(tmp_path, world):
+    shm_before = set(Path("/dev/shm").glob("golhip_bench_*"))
     mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
                        join=True, start_method="spawn")
     logs = [json.loads((tmp_path / f"rank{r}.log").read_text()) for r in range(world)]
@@ -216,4 +218,7 @@ def test_bench_rank_path_cpu(tmp_path, world):
     assert line["parity"] is not None and line["parity"]["turn"] == 25
     assert line["parity"]["ok"] and line["parity"]["cold_start_ok"], line["parity"]
     assert line["parity"]["digest_ok"] is True, line["parity"]
+    # every rank on this node: the timed region's barriers through shared memory, file removed
+    assert line["process"]["barrier"] == "shared memory", line["process"]
+    assert set(Path("/dev/shm").glob("golhip_bench_*")) <= shm_before
     assert line["untimed_generations_before_value"] == 5 + 25 + line["cold_start"]["preheat_turns"]

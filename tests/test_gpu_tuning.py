@@ -146,7 +146,10 @@ SLAB_CONFIGS = [(8, 8, 4), (8, 8, 8), (12, 8, 8), (16, 8, 8), (16, 8, 12), (16, 
                 (16, 14, 6, 2),
                 # gol_slab2 (NC = 9: the edge hand-off off the critical path)
                 (16, 8, 12, 9), (16, 12, 8, 9), (16, 12, 7, 9), (8, 8, 8, 9), (12, 8, 8, 9),
-                (16, 16, 5, 9), (16, 8, 8, 9)]
+                (16, 16, 5, 9), (16, 8, 8, 9),
+                # gol_slab3 (NC = 10: gol_slab2 pipelined across generations)
+                (16, 8, 12, 10), (16, 16, 6, 10), (16, 12, 8, 10), (16, 12, 7, 10), (16, 10, 8, 10),
+                (16, 8, 10, 10)]
 
 
 @pytest.mark.parametrize("cfg", SLAB_CONFIGS)
@@ -188,10 +191,12 @@ def test_register_slab_tracked_flips(golhip, tuning, oracle, monkeypatch):
     assert got == oracle.flips(before, exp)
 
 
-@pytest.mark.parametrize("code,k", [(90812, 16), (91208, 16), (91207, 16), (90808, 8), (90808, 12)])
+@pytest.mark.parametrize("code,k", [(90812, 16), (91208, 16), (91207, 16), (90808, 8), (90808, 12),
+                                    (100812, 16), (101208, 16), (101207, 16), (101606, 16)])
 def test_slab2_flips_ring_every_turn(golhip, tuning, oracle, monkeypatch, code, k):
-    """gol_slab2 writing EVERY generation's flips into the per-turn ring (golhip_step_flips) on
-    its production-candidate shapes, with counts: every turn's cells and count vs the oracle."""
+    """gol_slab2 / gol_slab3 writing EVERY generation's flips into the per-turn ring
+    (golhip_step_flips) on their production-candidate shapes, with counts: every turn's cells and
+    count vs the oracle."""
     monkeypatch.setenv("GOLHIP_SLAB", str(code))
     h, w = 300, 1000
     rng = np.random.default_rng(code)
