@@ -906,12 +906,15 @@ void halo_plan(int world, int rank, int64_t rows, int K, golhip_xfer out[4]) {
 //  * rank mode (one process per GPU): RCCL send/recv over xGMI, the plan above in one group;
 //  * single process (golhip_create / golhip_create_strips): every strip pulls its two halos from
 //    its neighbours' rows with peer copies (xGMI between devices, a D2D copy on one device).
-int exchange_halos(golhip_t h, int K) {
+// record_ready = false: the caller recorded ev_ready (the end of the previous block) itself, before
+// enqueueing this block's interior (step_block's interior-first order).
+int exchange_halos(golhip_t h, int K, bool record_ready = true) {
     const size_t bytes = (size_t)K * (size_t)h->pitch * sizeof(uint32_t);
-    for (auto &s : h->shards) {
-        HIPCHK(h, hipSetDevice(s.device));
-        HIPCHK(h, hipEventRecord(s.ev_ready, s.compute));
-    }
+    if (record_ready)
+        for (auto &s : h->shards) {
+            HIPCHK(h, hipSetDevice(s.device));
+            HIPCHK(h, hipEventRecord(s.ev_ready, s.compute));
+        }
     if (h->host_comm_on) {
         // host transport: stage the two sends through pinned host memory (after the block that
         // wrote them), hand the ordered plan to the caller, copy the two halos back on the comm
@@ -1002,7 +1005,13 @@ int exchange_halos(golhip_t h, int K) {
 // ring slot t (the launch's last generation's flips are written beside its output).
 constexpr int64_t kDiffNone = -1, kDiffLast = -2;
 int step_block(golhip_t h, int K, int64_t slot_gen, int64_t diff_slot = kDiffNone) {
-    if (h->split) {
+    // Rank mode over RCCL: the interior needs no halo and touches nothing the exchange does (it
+    // reads rows [0, rows), the receives write the halo rows, it writes the other buffer), so it
+    // is enqueued FIRST: the host's RCCL group set-up (~15 us, ncclGroupEnd) then runs while the
+    // interior does, instead of in front of it (profiles/r04/r04q_tail20_ring.txt).
+    const bool interior_first = h->split && h->rank_mode && !h->host_comm_on && !h->edge_first &&
+                                h->shards.size() == 1 && h->shards[0].rows >= 3 * K;
+    if (h->split && !interior_first) {
         int rc = exchange_halos(h, K);
         if (rc) return rc;
     }
@@ -1056,8 +1065,14 @@ int step_block(golhip_t h, int K, int64_t slot_gen, int64_t diff_slot = kDiffNon
             // wrote: with the early exchange the halo event no longer implies it (ev_ready marks
             // the compute stream at the end of the previous block).  Submission order (interior
             // first by default; edge_first: tuning A/B) only matters when both are ready at once
-            if (!h->edge_first)
+            if (interior_first) {
+                HIPCHK(h, hipEventRecord(s.ev_ready, s.compute));  // the end of the previous block
                 HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, pi, slots, s.compute));
+                int rc = exchange_halos(h, K, false);
+                if (rc) return rc;
+            } else if (!h->edge_first) {
+                HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, pi, slots, s.compute));
+            }
             HIPCHK(h, hipStreamWaitEvent(s.edge, s.ev_ready, 0));
             HIPCHK(h, hipStreamWaitEvent(s.edge, s.ev_halo, 0));
             HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, pb, slots, s.edge));

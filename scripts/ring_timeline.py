@@ -47,6 +47,19 @@ if sys.argv[1] == "run":
     sys.exit(0)
 
 d = sys.argv[1]
+if len(sys.argv) > 2 and sys.argv[2] == "tail":  # the last N dispatches, raw
+    n = int(sys.argv[3])
+    rows = []
+    for f in glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"][:60],
+                         r.get("Grid_Size_X", r.get("Grid_Size", "")), r.get("Queue_Id", "")))
+    rows.sort()
+    rows = rows[-n:]
+    t0 = rows[0][0]
+    for s_, e_, nm, g, q in rows:
+        print(f"{(s_ - t0) / 1e3:9.2f} .. {(e_ - t0) / 1e3:9.2f}  ({(e_ - s_) / 1e3:7.2f} us)  q{q} g{g}  {nm}")
+    sys.exit(0)
 nprint = int(sys.argv[2]) if len(sys.argv) > 2 else 6
 nlast = int(sys.argv[3]) if len(sys.argv) > 3 else 70
 rows = []
