@@ -505,7 +505,7 @@ int setup_engine(golhip_t h, int width, int height, int world, int k) {
 // Largest supported launch depth <= n.
 int pick_k(int n) {
     int kk = 1;
-    for (int c : {32, 16, 14, 12, 10, 8, 6, 4, 2, 1})
+    for (int c : {32, 24, 20, 16, 14, 12, 10, 8, 6, 4, 2, 1})  // 24 / 20: tuning build only
         if (c <= n && golhip::stencil_k_supported(c)) {
             kk = c;
             break;

@@ -125,7 +125,12 @@ inline int chunk_words(int K, int variant, bool counting = false) {
 }
 
 // Launch depths with a stencil instantiation, one translation unit each (stencil_k<K>.hip).
+#ifdef GOLHIP_TUNING
+// + K = 20 / 24 (the 62-word drift geometry; measured for the driver's 20-turn region)
+#define GOLHIP_STENCIL_DEPTHS(X) X(1) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(20) X(24) X(32)
+#else
 #define GOLHIP_STENCIL_DEPTHS(X) X(1) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(32)
+#endif
 #define GOLHIP_X(K)                                                                           \
     hipError_t launch_stencil_k##K(int variant, const uint32_t *in, uint32_t *out,            \
                                    const StencilParams &p, unsigned long long *slots,        \

@@ -55,6 +55,23 @@ def test_every_kernel_variant(golhip, tuning, oracle, monkeypatch, variant, k):
             assert np.array_equal(counts.astype(np.int64), exp_counts), (variant, k, h, w, band)
 
 
+@pytest.mark.parametrize("variant", ["prod", "drift62"])
+@pytest.mark.parametrize("k", [20, 24])
+def test_tuning_depths_20_24(golhip, tuning, oracle, monkeypatch, variant, k):
+    """The tuning build's extra launch depths K = 20 / 24 (62-word drift geometry; measured for the
+    driver's 20-turn region as one launch): exactly k deep, counts, wrap, partial chunks."""
+    monkeypatch.setenv("GOLHIP_VARIANT", variant)
+    for (h, w) in [(64, 4160), (35, 2016), (130, 8192), (20, 1984)]:
+        rng = np.random.default_rng(h * 13 + w + k)
+        board = ((rng.random((h, w)) < 0.37) * 255).astype(np.uint8)
+        turns = 2 * k + 3
+        exp, exp_counts = oracle.packed_run(board, turns)
+        for band in (0, 40):
+            out, counts, cells, count = run_engine(golhip, board, turns, k=k, counts=True, band_rows=band, lib=tuning)
+            assert np.array_equal(out, exp), (k, h, w, band)
+            assert np.array_equal(counts.astype(np.int64), exp_counts), (k, h, w, band)
+
+
 @pytest.mark.parametrize("variant", ["driftlds", "driftzip", "drift62", "pre63", "prodmask"])
 @pytest.mark.parametrize("k", [2, 4, 6, 8, 10, 12, 14, 16, 32])
 def test_drift_variant_every_k(golhip, tuning, oracle, monkeypatch, variant, k):
