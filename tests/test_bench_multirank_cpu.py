@@ -154,7 +154,7 @@ class FakeEngine:
         FakeEngine.log.append(("close",))
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, extra=()):
     for p in (str(ROOT), str(ROOT / "oracle"), str(PKG)):
         if p not in sys.path:
             sys.path.insert(0, p)
@@ -172,7 +172,7 @@ def _worker(rank, world, port, out_dir):
 
     sys.argv = ["bench.py", "--gpus", str(world), "--steps", "20", "--warmup", "5",
                 "--size", "4096", "--strong-size", "2048", "--strong-steps", "32",
-                "--preheat-ms", "50"]
+                "--preheat-ms", "50", *extra]
     out = os.path.join(out_dir, f"rank{rank}.out")
     with open(out, "w") as f:
         so = sys.stdout
@@ -222,3 +222,64 @@ def test_bench_rank_path_cpu(tmp_path, world):
     assert line["process"]["barrier"] == "shared memory", line["process"]
     assert set(Path("/dev/shm").glob("golhip_bench_*")) <= shm_before
     assert line["untimed_generations_before_value"] == 5 + 25 + line["cold_start"]["preheat_turns"]
+
+
+def test_bench_rank_path_cpu_process_group_barrier(tmp_path):
+    """--rccl-barrier: the timed region between the process group's barriers (here gloo) even when
+    every rank is on this node; the same line otherwise."""
+    mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path), ("--rccl-barrier",)), nprocs=2,
+                       join=True, start_method="spawn")
+    line = json.loads((tmp_path / "rank0.out").read_text().strip().splitlines()[0])
+    assert line["process"]["barrier"] == "gloo", line["process"]
+    assert line["parity"]["ok"] and line["parity"]["digest_ok"] is True, line["parity"]
+
+
+def _barrier_worker(rank, world, port, out_dir):
+    for p in (str(ROOT), str(PKG)):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import time
+
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    import bench
+
+    b = bench.ShmBarrier(rank, world, timeout_s=2.0)
+    order = []
+    for i in range(3):  # a barrier holds every rank until all have arrived
+        if rank == world - 1:
+            time.sleep(0.2)
+        b.wait()
+        order.append(time.time())
+    result = {"ok_waits": 3, "times": order}
+    if rank == 0:  # the other ranks never arrive at a 4th barrier: rank 0 fails at the deadline
+        t = time.perf_counter()
+        try:
+            b.wait()
+            result["timeout"] = None
+        except RuntimeError as e:
+            result["timeout"] = str(e)
+        result["waited"] = time.perf_counter() - t
+    dist.barrier()
+    b.close()
+    with open(os.path.join(out_dir, f"b{rank}.json"), "w") as f:
+        json.dump(result, f)
+    dist.destroy_process_group()
+
+
+def test_shm_barrier_holds_ranks_and_times_out(tmp_path):
+    """bench.ShmBarrier: no rank leaves a barrier before every rank has arrived (the late rank's
+    0.2 s delay shows in every rank's exit time), and a rank whose peer never arrives fails at the
+    deadline naming the missing ranks."""
+    world = 3
+    shm_before = set(Path("/dev/shm").glob("golhip_bench_*"))
+    mp.start_processes(_barrier_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    res = [json.loads((tmp_path / f"b{r}.json").read_text()) for r in range(world)]
+    for i in range(3):
+        exits = [r["times"][i] for r in res]
+        assert max(exits) - min(exits) < 0.15, exits  # released together, after the late rank
+    assert res[0]["timeout"] and "ranks [1, 2] did not arrive" in res[0]["timeout"], res[0]
+    assert 1.9 <= res[0]["waited"] < 10, res[0]
+    assert set(Path("/dev/shm").glob("golhip_bench_*")) <= shm_before
