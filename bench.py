@@ -167,26 +167,47 @@ class ShmBarrier:
     world 1: profiles/r04/r04l_rank_rehearsal.log).  Set up and torn down outside the timed
     region; the file is unlinked as soon as every rank has mapped it."""
 
-    def __init__(self, rank: int, world: int, timeout_s: float):
-        import mmap
+    def __init__(self, rank: int, world: int, timeout_s: float, path: str, mm, fd: int):
         import struct
         self.struct, self.rank, self.world, self.timeout_s, self.gen = struct, rank, world, timeout_s, 0
+        self.path, self.mm, self.fd = path, mm, fd
+
+    @classmethod
+    def create(cls, rank: int, world: int, timeout_s: float) -> "ShmBarrier | None":
+        """Collective: every rank maps the page, or every rank gets None (a rank that cannot create
+        or map it -- no /dev/shm, a full one -- and the others then keep the process group's barrier
+        too, so the ranks never disagree on which barrier they wait in)."""
+        import mmap
         name = [f"/dev/shm/golhip_bench_{os.getpid()}_{time.time_ns()}" if rank == 0 else None]
         if world > 1:
             dist.broadcast_object_list(name, src=0)
-        self.path = name[0]
-        size = 64 * world
+        path, size, ok, mm, fd = name[0], 64 * world, True, None, -1
         if rank == 0:
-            with open(self.path, "wb") as f:
-                f.write(b"\0" * size)
+            try:
+                with open(path, "wb") as f:
+                    f.write(b"\0" * size)
+            except OSError:
+                ok = False
         if world > 1:
-            dist.barrier()
-        self.fd = os.open(self.path, os.O_RDWR)
-        self.mm = mmap.mmap(self.fd, size)
+            barrier()
+        try:
+            fd = os.open(path, os.O_RDWR)
+            mm = mmap.mmap(fd, size)
+        except (OSError, ValueError):
+            ok = False
+        oks = [ok]
         if world > 1:
-            dist.barrier()
-        if rank == 0:
-            os.unlink(self.path)
+            oks = [None] * world
+            dist.all_gather_object(oks, ok)
+        if rank == 0 and os.path.exists(path):
+            os.unlink(path)  # every rank has mapped it (or given up): the page lives on in the maps
+        if all(oks):
+            return cls(rank, world, timeout_s, path, mm, fd)
+        if mm is not None:
+            mm.close()
+        if fd >= 0:
+            os.close(fd)
+        return None
 
     def wait(self):
         self.gen += 1
@@ -588,7 +609,7 @@ def main():
         # barriers go through shared memory (--rccl-barrier keeps the process group's)
         if (not a.rccl_barrier and int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) == world
                 and os.path.isdir("/dev/shm")):
-            SHM_BARRIER = ShmBarrier(rank, world, a.pg_timeout_s)
+            SHM_BARRIER = ShmBarrier.create(rank, world, a.pg_timeout_s)
     golhip.set_default_comm_timeout(a.comm_timeout_ms)
 
     width = a.size

@@ -245,7 +245,8 @@ def _barrier_worker(rank, world, port, out_dir):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     import bench
 
-    b = bench.ShmBarrier(rank, world, timeout_s=2.0)
+    b = bench.ShmBarrier.create(rank, world, timeout_s=2.0)
+    assert b is not None
     order = []
     for i in range(3):  # a barrier holds every rank until all have arrived
         if rank == world - 1:
@@ -282,4 +283,40 @@ def test_shm_barrier_holds_ranks_and_times_out(tmp_path):
         assert max(exits) - min(exits) < 0.15, exits  # released together, after the late rank
     assert res[0]["timeout"] and "ranks [1, 2] did not arrive" in res[0]["timeout"], res[0]
     assert 1.9 <= res[0]["waited"] < 10, res[0]
+    assert set(Path("/dev/shm").glob("golhip_bench_*")) <= shm_before
+
+
+def _fallback_worker(rank, world, port, out_dir):
+    for p in (str(ROOT), str(PKG)):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    import bench
+
+    if rank == 1:  # this rank cannot map the page
+        real_open = os.open
+
+        def failing_open(path, *a, **k):
+            if "golhip_bench_" in str(path):
+                raise OSError("no shared memory here")
+            return real_open(path, *a, **k)
+
+        os.open = failing_open
+    b = bench.ShmBarrier.create(rank, world, timeout_s=2.0)
+    with open(os.path.join(out_dir, f"f{rank}.json"), "w") as f:
+        json.dump({"barrier": b is not None}, f)
+    dist.destroy_process_group()
+
+
+def test_shm_barrier_all_or_none(tmp_path):
+    """One rank that cannot map the page makes EVERY rank keep the process group's barrier (the
+    ranks must not wait in different barriers), and no file is left behind."""
+    world = 3
+    shm_before = set(Path("/dev/shm").glob("golhip_bench_*"))
+    mp.start_processes(_fallback_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    res = [json.loads((tmp_path / f"f{r}.json").read_text()) for r in range(world)]
+    assert [r["barrier"] for r in res] == [False] * world, res
     assert set(Path("/dev/shm").glob("golhip_bench_*")) <= shm_before
