@@ -761,7 +761,12 @@ RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K, bool counting) 
     // checked): with counts 8 x 12 0.843 / 16 x 6 0.844 / 12 x 8 0.856 us/turn at 5120^2, without
     // counts 16 x 6 0.735 / 12 x 8 0.744 / 8 x 12 0.790; 4096^2 takes 12 x 7 either way (0.781 /
     // 0.662: 237 slabs, 21 rows per SIMD).
-    static constexpr Cand kCount16[] = {{8, 12, 9}, {16, 6, 9}, {12, 8, 9}, {12, 7, 9}};
+    // With counts the shapes whose pure-halo waves used to flush a generation after every barrier
+    // (2S <= K: 16 x 6, 12 x 7, 12 x 8) flush every generation at the end of the launch instead
+    // (NC = 12): the per-barrier flush sat on each generation's critical path -- 5120^2 16 x 6
+    // 0.852 -> 0.772 us/turn, 4096^2 12 x 7 0.782 -> 0.730 (profiles/r04/r04u_tune.log; moving
+    // the 8 x 12 flush INTO the loop instead cost 0.844 -> 0.945, r04t).
+    static constexpr Cand kCount16[] = {{16, 6, 12}, {8, 12, 9}, {12, 8, 12}, {12, 7, 12}};
     static constexpr Cand kPlain16[] = {{16, 6, 9}, {12, 8, 9}, {8, 12, 9}, {12, 7, 9}};
     static constexpr Cand kOther[] = {{8, 8, 4}};
     const Cand *cands = K == 16 ? (counting ? kCount16 : kPlain16) : kOther;
@@ -1040,7 +1045,7 @@ int step_block(golhip_t h, int K, int64_t slot_gen, int64_t diff_slot = kDiffNon
             } else if (h->stamp_buf && !diff && K > 1) {
                 // gol_slab2 writes its phase stamps through p.stamp (never p.diff)
                 const RegKernel rk = pick_reg_kernel(h, s.rows, K, slots != nullptr);
-                if (rk.kind == 3 && (rk.NC == 9 || rk.NC == 10) /* gol_slab2 / gol_slab3 */ &&
+                if (rk.kind == 3 && (rk.NC >= 9 && rk.NC <= 12) /* gol_slab2 / gol_slab3 */ &&
                     8 * p.nbands * (int64_t)p.nchunks * rk.W <= 4 * kStampWaves) {
                     p.stamp = h->stamp_buf;
                     h->stamp_waves = p.nbands * (int64_t)p.nchunks * rk.W;

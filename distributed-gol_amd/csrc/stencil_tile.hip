@@ -591,7 +591,11 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
 //      so they run while the neighbours are still publishing;
 //   4. the barrier, the neighbours' edge sums from LDS, and the two edge rows.
 // Only step 4's short tail (an LDS read and two 7-op rules) waits on the other waves.
-template <int K, int W, int S, bool COUNT, int LD>
+// FM, where the per-generation counts are flushed (tuning A/B): 0 (production) the pure-halo waves
+// flush generation g - 2 after every barrier when there are two per side (2S <= K), else every
+// generation at the end of the launch; 1 (NC = 11) in the loop whenever there is one per side
+// (S <= K); 2 (NC = 12) always at the end.
+template <int K, int W, int S, bool COUNT, int LD, int FM = 0>
 __global__ __launch_bounds__(64 * W) void gol_slab2(const uint32_t *__restrict__ in,
                                                     uint32_t *__restrict__ out, StencilParams p,
                                                     unsigned long long *__restrict__ slots) {
@@ -654,7 +658,7 @@ __global__ __launch_bounds__(64 * W) void gol_slab2(const uint32_t *__restrict__
     // with 2S <= K the two halo waves take turns flushing the generation that is complete after
     // generation g's barrier (g - 2, 0-based), as gol_slab does
     auto flush_after_barrier = [&](int g) {
-        if constexpr (COUNT && 2 * S <= K) {
+        if constexpr (COUNT && (FM == 0 ? 2 * S <= K : FM == 1 ? S <= K : false)) {
             if (g >= 2 && w == ((g & 1) ? W - 1 : 0)) {
                 uint32_t acc[1] = {cnt_sum(g - 2)};
                 flush_counts<1>(acc, g - 2, lane, group, slots);
@@ -781,7 +785,7 @@ __global__ __launch_bounds__(64 * W) void gol_slab2(const uint32_t *__restrict__
         if (p.stamp) st_t2 = __builtin_amdgcn_s_memrealtime();
     if constexpr (COUNT) {  // the generations not flushed yet
         lds_barrier();
-        if constexpr (2 * S <= K) {
+        if constexpr (FM == 0 ? 2 * S <= K : FM == 1 ? S <= K : false) {
             if (w == ((K & 1) ? 0 : W - 1)) {
                 uint32_t acc[1] = {cnt_sum(K - 1)};
                 flush_counts<1>(acc, K - 1, lane, group, slots);
@@ -1084,13 +1088,16 @@ hipError_t launch_tile_kt(const uint32_t *in, uint32_t *out, const StencilParams
 // flips variant (LD = 2).  NC = kSlab2 selects gol_slab2 (the edge hand-off off the critical path).
 constexpr int kSlab2 = 9;
 constexpr int kSlab3 = 10;  // gol_slab3: gol_slab2 pipelined across generations
+constexpr int kSlab2F = 11;  // gol_slab2, counts flushed in the launch whenever S <= K (FM = 1)
+constexpr int kSlab2E = 12;  // gol_slab2, counts flushed at the end of the launch (FM = 2)
 constexpr bool slab_prod_ws(int K, int W, int S) {
     return (K == 16 && W == 8 && S == 12) || (K == 16 && W == 12 && S == 8) ||
            (K == 16 && W == 12 && S == 7) || (K == 16 && W == 16 && S == 6) || (K == 8 && W == 8 && S == 8) ||
            (K == 12 && W == 8 && S == 8);
 }
 constexpr bool slab_prod_shape(int K, int W, int S, int NC) {
-    return slab_prod_ws(K, W, S) && (NC == kSlab2 || NC == kSlab3 || (K == 16 ? NC == 2 : NC == 4));
+    return slab_prod_ws(K, W, S) &&
+           (NC == kSlab2 || NC == kSlab3 || NC == kSlab2F || NC == kSlab2E || (K == 16 ? NC == 2 : NC == 4));
 }
 
 template <int K, int W, int S, int NC>
@@ -1120,6 +1127,30 @@ hipError_t launch_slab_kws(const uint32_t *in, uint32_t *out, const StencilParam
             hipLaunchKernelGGL((gol_slab3<K, W, S, true, 0>), dim3(blocks), block, 0, s, in, out, p, slots);
         else
             hipLaunchKernelGGL((gol_slab3<K, W, S, false, 0>), dim3(blocks), block, 0, s, in, out, p, slots);
+        return hipGetLastError();
+    }
+    if constexpr (NC == kSlab2F || NC == kSlab2E) {
+        constexpr int FM = NC - 10;
+        if (p.diff && p.diff_stride > 0) {
+            if constexpr (slab_prod_shape(K, W, S, NC)) {
+                if (slots)
+                    hipLaunchKernelGGL((gol_slab2<K, W, S, true, 2, FM>), dim3(blocks), block, 0, s, in, out, p, slots);
+                else
+                    hipLaunchKernelGGL((gol_slab2<K, W, S, false, 2, FM>), dim3(blocks), block, 0, s, in, out, p, slots);
+                return hipGetLastError();
+            } else {
+                return hipErrorNotSupported;
+            }
+        }
+        const int ld = p.diff ? 1 : 0;
+        if (ld && slots)
+            hipLaunchKernelGGL((gol_slab2<K, W, S, true, 1, FM>), dim3(blocks), block, 0, s, in, out, p, slots);
+        else if (ld)
+            hipLaunchKernelGGL((gol_slab2<K, W, S, false, 1, FM>), dim3(blocks), block, 0, s, in, out, p, slots);
+        else if (slots)
+            hipLaunchKernelGGL((gol_slab2<K, W, S, true, 0, FM>), dim3(blocks), block, 0, s, in, out, p, slots);
+        else
+            hipLaunchKernelGGL((gol_slab2<K, W, S, false, 0, FM>), dim3(blocks), block, 0, s, in, out, p, slots);
         return hipGetLastError();
     }
     if constexpr (NC == kSlab2) {
@@ -1175,16 +1206,21 @@ hipError_t launch_slab_kws(const uint32_t *in, uint32_t *out, const StencilParam
 // slab_prod_shape above) in both builds; the tuning build adds the neighbours kept measurable
 // (profiles/r02/small_boards.txt, profiles/r03/r03e_tune_slab.log) and the register-tile kernel.
 // Round 4: K = 16 runs gol_slab2 (NC = 9) in production (configs[1] 5120^2 with every count 0.908
-// -> 0.843 us/turn, configs[4]-sized 4096^2 0.829 -> 0.781; profiles/r04/r04c_tune_slab.log).
+// -> 0.843 us/turn, configs[4]-sized 4096^2 0.829 -> 0.781; profiles/r04/r04c_tune_slab.log), and
+// with counts gol_slab2 flushing every generation's count at the end of the launch (NC = 12: 0.772
+// at 5120^2 with 16 x 6, 0.730 at 4096^2 with 12 x 7; profiles/r04/r04u_tune.log).
 #define GOLHIP_SLAB_PROD_CONFIGS(X) \
-    X(8, 8, 8, 4) X(12, 8, 8, 4) X(16, 8, 12, 9) X(16, 16, 6, 9) X(16, 12, 8, 9) X(16, 12, 7, 9)
+    X(8, 8, 8, 4) X(12, 8, 8, 4) X(16, 8, 12, 9) X(16, 16, 6, 9) X(16, 12, 8, 9) X(16, 12, 7, 9) \
+    X(16, 16, 6, 12) X(16, 12, 7, 12) X(16, 12, 8, 12)
 #ifdef GOLHIP_TUNING
 #define GOLHIP_SLAB_CONFIGS(X) GOLHIP_SLAB_PROD_CONFIGS(X) \
     X(16, 8, 12, 2) X(16, 12, 8, 2) X(16, 12, 7, 2) \
     X(8, 8, 4, 4) X(16, 8, 8, 4) X(16, 8, 12, 4) X(16, 16, 8, 4) \
     X(16, 12, 8, 4) X(16, 10, 8, 2) X(16, 14, 6, 2) X(16, 16, 6, 2) X(16, 16, 5, 2) \
     X(8, 8, 8, 9) X(12, 8, 8, 9) X(16, 16, 5, 9) X(16, 10, 8, 9) X(16, 8, 8, 9) X(16, 12, 6, 9) \
-    X(16, 8, 12, 10) X(16, 16, 6, 10) X(16, 12, 8, 10) X(16, 12, 7, 10) X(16, 10, 8, 10) X(16, 8, 10, 10)
+    X(16, 8, 12, 10) X(16, 16, 6, 10) X(16, 12, 8, 10) X(16, 12, 7, 10) X(16, 10, 8, 10) X(16, 8, 10, 10) \
+    X(16, 8, 12, 11) X(16, 8, 10, 11) X(16, 10, 8, 11) X(16, 12, 8, 11) \
+    X(16, 16, 5, 12)
 #define GOLHIP_TILE_CONFIGS(X) \
     X(2, 16) X(4, 8) X(4, 16) X(4, 32) X(6, 16) X(8, 8) X(8, 16) X(8, 32) X(10, 16) X(12, 8) \
     X(12, 16) X(12, 32) X(14, 16) X(16, 8) X(16, 16) X(16, 32)

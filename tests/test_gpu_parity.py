@@ -457,17 +457,18 @@ def test_count_window_flushes(golhip, oracle, k):
 def test_small_board_picks_register_slab(golhip, oracle):
     """configs[1]-sized boards take the register-slab path automatically (with the planner's own
     depth choice); results unchanged, counts every turn."""
-    # the shape model (pick_reg_kernel) over the gol_slab2 shapes (NC = 9): configs[1] 5120^2 takes
-    # 8 x 12 with counts and 16 x 6 without (240 slabs, 24 rows per SIMD either way; the measured
-    # order breaks the tie), configs[4] 4096^2 takes 12 x 7 (237 slabs, 21 rows per SIMD)
+    # the shape model (pick_reg_kernel) over the gol_slab2 shapes: configs[1] 5120^2 takes 16 x 6
+    # (240 slabs, 24 rows per SIMD; the measured order breaks the tie with 8 x 12 / 12 x 8), with
+    # counts flushed at the end of the launch (NC = 12); configs[4] 4096^2 takes 12 x 7 (237 slabs,
+    # 21 rows per SIMD), the same way with counts
     with golhip.Engine(5120, 5120, k=16) as e:
         assert e.launch_kind(16) == ("slab", 91606)
-        assert e.launch_kind(16, counts=True) == ("slab", 90812)
+        assert e.launch_kind(16, counts=True) == ("slab", 121606)
         assert e.launch_kind(8) == ("slab", 808)
         assert e.launch_kind(8, counts=True) == ("slab", 808)
     with golhip.Engine(4096, 4096, k=16) as e:
         assert e.launch_kind(16) == ("slab", 91207)
-        assert e.launch_kind(16, counts=True) == ("slab", 91207)
+        assert e.launch_kind(16, counts=True) == ("slab", 121207)
     words = oracle.init_random(5120, 512, seed=2)
     with golhip.Engine(5120, 512, k=16) as e:
         assert e.launch_kind(16, counts=True)[0] == "slab"
