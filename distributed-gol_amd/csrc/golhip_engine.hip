@@ -1045,7 +1045,7 @@ int step_block(golhip_t h, int K, int64_t slot_gen, int64_t diff_slot = kDiffNon
             } else if (h->stamp_buf && !diff && K > 1) {
                 // gol_slab2 writes its phase stamps through p.stamp (never p.diff)
                 const RegKernel rk = pick_reg_kernel(h, s.rows, K, slots != nullptr);
-                if (rk.kind == 3 && (rk.NC >= 9 && rk.NC <= 12) /* gol_slab2 / gol_slab3 */ &&
+                if (rk.kind == 3 && (rk.NC >= 9 && rk.NC <= 13) /* gol_slab2 / gol_slab3 */ &&
                     8 * p.nbands * (int64_t)p.nchunks * rk.W <= 4 * kStampWaves) {
                     p.stamp = h->stamp_buf;
                     h->stamp_waves = p.nbands * (int64_t)p.nchunks * rk.W;

@@ -170,7 +170,9 @@ SLAB_CONFIGS = [(8, 8, 4), (8, 8, 8), (12, 8, 8), (16, 8, 8), (16, 8, 12), (16, 
                 # gol_slab2 with the in-launch count flush whenever S <= K (NC = 11)
                 (16, 8, 12, 11), (16, 8, 10, 11), (16, 10, 8, 11), (16, 12, 8, 11),
                 # ... and with every generation's counts flushed at the end (NC = 12)
-                (16, 12, 7, 12), (16, 12, 8, 12), (16, 16, 6, 12), (16, 16, 5, 12)]
+                (16, 12, 7, 12), (16, 12, 8, 12), (16, 16, 6, 12), (16, 16, 5, 12),
+                # ... with the younger half of the waves at s_setprio 1 (NC = 13)
+                (16, 16, 6, 13), (16, 12, 7, 13), (16, 8, 12, 13)]
 
 
 @pytest.mark.parametrize("cfg", SLAB_CONFIGS)
@@ -213,7 +215,7 @@ def test_register_slab_tracked_flips(golhip, tuning, oracle, monkeypatch):
 
 
 @pytest.mark.parametrize("code,k", [(90812, 16), (91208, 16), (91207, 16), (90808, 8), (90808, 12),
-                                    (100812, 16), (101208, 16), (101207, 16), (101606, 16), (110812, 16), (121207, 16), (121606, 16)])
+                                    (100812, 16), (101208, 16), (101207, 16), (101606, 16), (110812, 16), (121207, 16), (121606, 16), (131606, 16)])
 def test_slab2_flips_ring_every_turn(golhip, tuning, oracle, monkeypatch, code, k):
     """gol_slab2 / gol_slab3 writing EVERY generation's flips into the per-turn ring
     (golhip_step_flips) on their production-candidate shapes, with counts: every turn's cells and
