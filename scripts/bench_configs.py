@@ -10,7 +10,6 @@
 Prints one JSON object.  Run on the GPU box from the repo root.
 """
 import json
-import os
 import subprocess
 import sys
 import tempfile

@@ -15,7 +15,6 @@ import glob
 import json
 import sys
 from collections import defaultdict
-from pathlib import Path
 
 
 def load(d):

@@ -6,7 +6,6 @@ Prints one JSON object.  Run on the GPU box from the repo root."""
 import json
 import sys
 import time
-import zlib
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
