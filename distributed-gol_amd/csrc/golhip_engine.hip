@@ -38,6 +38,7 @@ constexpr int kVersion = 101;
 // least the graph length kGraphGens: tests shrink it to exercise flushes).
 constexpr int kCountWindowDefault = 4096;
 constexpr int kCountWindowMin = 128;
+constexpr bool kTuningBuildEngine = golhip::kTuningBuild;
 constexpr int64_t kStampWaves = 1 << 20;  // tuning build: waves of the per-wave stamp buffer
 // Default deadline of a host wait on RCCL-dependent work and of the communicator's set-up
 // (golhip_set_comm_timeout(NULL, ms) changes it for later creates): well under the 600 s a driver
@@ -52,6 +53,10 @@ struct Shard {
     hipStream_t compute = nullptr, comm = nullptr;
     hipStream_t edge = nullptr;  // boundary bands of a split board, concurrent with the interior
     hipEvent_t ev_ready = nullptr, ev_halo = nullptr, ev_edge = nullptr;
+    // tuning (GOLHIP_JOIN=1): the split step's join of the boundary bands as a stream write/wait
+    // of a device word instead of an event wait
+    uint32_t *join_flag = nullptr;
+    uint32_t join_seq = 0;
     uint32_t *buf[2] = {nullptr, nullptr};  // allocation base (halo rows first)
     unsigned long long *slots = nullptr;    // count_window x kCountSlots
     unsigned long long *scratch_u64 = nullptr;
@@ -127,6 +132,7 @@ struct golhip_engine {
     // the boundary bands' waves raise their issue priority (StencilParams::prio); tuning knob
     // GOLHIP_EDGE_SETPRIO=0 turns it off for A/B
     int edge_setprio = 1;
+    int join_mode = 0;  // tuning (GOLHIP_JOIN): 0 event wait, 1 stream write/wait of a device word
     int graph_mode = -1;  // golhip_set_graphs: -1 automatic, 0 never, 1 whenever the plan allows
     // RCCL fail-fast (rank mode): every host wait on work that can depend on an RCCL transfer polls
     // ncclCommGetAsyncError against a deadline and fails the handle when it passes
@@ -363,6 +369,10 @@ int alloc_shard(golhip_t h, Shard &s) {
     HIPCHK(h, hipEventCreateWithFlags(&s.ev_ready, hipEventDisableTiming));
     HIPCHK(h, hipEventCreateWithFlags(&s.ev_halo, hipEventDisableTiming));
     HIPCHK(h, hipEventCreateWithFlags(&s.ev_edge, hipEventDisableTiming));
+    if (kTuningBuildEngine) {
+        HIPCHK(h, hipMalloc(&s.join_flag, sizeof(uint32_t)));
+        HIPCHK(h, hipMemsetAsync(s.join_flag, 0, sizeof(uint32_t), s.compute));
+    }
     const size_t words = (size_t)(s.rows + 2 * (int64_t)h->halo) * (size_t)h->pitch;
     for (int i = 0; i < 2; ++i) {
         HIPCHK(h, hipMalloc(&s.buf[i], words * sizeof(uint32_t)));
@@ -423,6 +433,7 @@ void free_shard(Shard &s, int64_t drain_ms = 0, bool comm_failed = false) {
     if (s.ev_ready) (void)hipEventDestroy(s.ev_ready);
     if (s.ev_halo) (void)hipEventDestroy(s.ev_halo);
     if (s.ev_edge) (void)hipEventDestroy(s.ev_edge);
+    if (s.join_flag) (void)hipFree(s.join_flag);
     if (s.compute) (void)hipStreamDestroy(s.compute);
     if (s.comm) (void)hipStreamDestroy(s.comm);
     if (s.edge) (void)hipStreamDestroy(s.edge);
@@ -481,6 +492,7 @@ int setup_engine(golhip_t h, int width, int height, int world, int k) {
     if (const char *e = std::getenv("GOLHIP_EDGE_PRIO")) h->edge_prio = std::atoi(e) != 0;
     if (const char *e = std::getenv("GOLHIP_EDGE_FIRST")) h->edge_first = std::atoi(e) != 0;
     if (const char *e = std::getenv("GOLHIP_EDGE_SETPRIO")) h->edge_setprio = std::atoi(e) != 0;
+    if (const char *e = std::getenv("GOLHIP_JOIN")) h->join_mode = std::atoi(e);
     if (const char *e = std::getenv("GOLHIP_VARIANT"))
         h->variant = std::strcmp(e, "chain") == 0     ? golhip::kVariantChain
                      : std::strcmp(e, "skew") == 0   ? golhip::kVariantSkew
@@ -1082,9 +1094,15 @@ int step_block(golhip_t h, int K, int64_t slot_gen, int64_t diff_slot = kDiffNon
             HIPCHK(h, hipStreamWaitEvent(s.edge, s.ev_halo, 0));
             HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, pb, slots, s.edge));
             HIPCHK(h, hipEventRecord(s.ev_edge, s.edge));
+            if (h->join_mode == 1 && s.join_flag)
+                HIPCHK(h, hipStreamWriteValue32(s.edge, s.join_flag, ++s.join_seq, 0));
             if (h->edge_first)
                 HIPCHK(h, golhip::launch_stencil(K, h->variant, in, out, pi, slots, s.compute));
-            HIPCHK(h, hipStreamWaitEvent(s.compute, s.ev_edge, 0));
+            if (h->join_mode == 1 && s.join_flag)
+                HIPCHK(h, hipStreamWaitValue32(s.compute, s.join_flag, s.join_seq, hipStreamWaitValueGte,
+                                               0xFFFFFFFFu));
+            else
+                HIPCHK(h, hipStreamWaitEvent(s.compute, s.ev_edge, 0));
             h->edge_k = K;
         } else {
             h->edge_k = 0;
