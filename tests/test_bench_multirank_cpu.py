@@ -1,4 +1,4 @@
-"""bench.py's N > 1 control flow on CPU: two and three gloo ranks run bench.main() exactly as
+"""bench.py's N > 1 control flow on CPU: two, three and eight gloo ranks run bench.main() exactly as
 `torch.distributed.run --nproc-per-node N bench.py --gpus N ...` would, with the GPU engine replaced
 by a host stand-in.  The driver's 8-GPU scaling run is the only place the RCCL rank path meets
 hardware, so this checks what can break there without a GPU: every rank makes the same collective
@@ -185,7 +185,7 @@ def _worker(rank, world, port, out_dir, extra=()):
         json.dump(FakeEngine.log, f)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_bench_rank_path_cpu(tmp_path, world):
     shm_before = set(Path("/dev/shm").glob("golhip_bench_*"))
     mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
