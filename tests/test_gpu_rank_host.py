@@ -147,3 +147,28 @@ def test_bench_rank_path_host_transport(tmp_path):
         assert line["parity"] is not None and line["parity"]["ok"], line["parity"]
         assert line["parity"]["cold_start_ok"]
         assert line["transport"].startswith("gloo host transport")
+
+
+@pytest.mark.timeout(300)
+def test_bench_rank_process_rehearsal_ring_of_one(tmp_path):
+    """What one rank of the driver's N > 1 run does, on this GPU: bench.py --pg-always creates the
+    torch process group over RCCL and runs its collectives at world 1, and GOLHIP_RING_SELF=1 makes
+    the engine the RCCL ring of one (the rank-mode split step, RCCL send/recv, the count
+    all-reduce); the timed region between shared-memory barriers.  The line's parity and the board
+    digest (8192 x 16384, seed 3, oracle goldens) must hold."""
+    env = dict(os.environ, GOLHIP_RING_SELF="1", PYTHONUNBUFFERED="1", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()))
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--pg-always", "--size", "8192", "--height", "16384",
+           "--steps", "20", "--warmup", "5", "--no-cpu", "--no-sweep", "--no-strong", "--no-configs",
+           "--no-flips", "--preheat-ms", "20"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    line = json.loads(lines[0])
+    (tmp_path / "rehearsal.json").write_text(lines[0])
+    assert line["transport"] == "rccl ring of one (GOLHIP_RING_SELF=1)", line["transport"]
+    assert line["process"]["process_group"] == "nccl" and line["process"]["barrier"] == "shared memory"
+    assert line["process"]["gpu_max_hw_queues"] == "8"
+    assert line["parity"]["ok"] and line["parity"]["cold_start_ok"], line["parity"]
+    assert line["parity"]["digest_ok"] is True, line["parity"]
