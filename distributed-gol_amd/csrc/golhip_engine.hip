@@ -39,6 +39,12 @@ constexpr int kVersion = 101;
 constexpr int kCountWindowDefault = 4096;
 constexpr int kCountWindowMin = 128;
 constexpr bool kTuningBuildEngine = golhip::kTuningBuild;
+// The register slab runs boards on which the streaming kernel would have at most this many
+// minimal-band (max(K, 8)-row) waves per CU.  Round 4 sweep (profiles/r04/r04mid_tune_mid.log,
+// 512 / 256 turns, every count equal): the slab is 7-11 % faster than streaming up to 16384^2
+// without counts (12288^2 2.82 vs 3.14 us/turn, 16384^2 4.09 vs 4.40), even at 20480^2, and
+// slower there with counts (9.33 vs 8.39); 16384^2 has 36 such waves per CU, 20480^2 55.
+constexpr int64_t kSlabMaxWaves1PerCu = 40;
 constexpr int64_t kStampWaves = 1 << 20;  // tuning build: waves of the per-wave stamp buffer
 // Default deadline of a host wait on RCCL-dependent work and of the communicator's set-up
 // (golhip_set_comm_timeout(NULL, ms) changes it for later creates): well under the 600 s a driver
@@ -738,8 +744,8 @@ RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K, bool counting) 
     // automatic: the slab shape measured best for this depth (profiles/r02/small_boards.txt: at
     // K = 16, 8 waves x 12 rows -- 64 output rows per slab, 240 slabs at 5120^2, about one per CU
     // -- 1.33 us per turn with counts vs 1.62 for the level split, 1.21 vs 1.35 at 4096^2, 2.45
-    // vs 2.87 at 8192^2), on boards where the streaming kernel has fewer than four minimal-band
-    // waves per SIMD
+    // vs 2.87 at 8192^2), on boards where the streaming kernel has at most kSlabMaxWaves1PerCu
+    // minimal-band waves per CU (round 4: 40, up from 16)
     // (2 row chains per wave at 8 x 12: 1 % over 4, fewer segment-start sums).  Counting
     // launches at K = 16 take 12 waves x 8 rows: its four pure-halo waves (2S <= K) skip the
     // counts and flush the other waves' per-generation sums during the launch (5120^2 with every
@@ -755,7 +761,7 @@ RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K, bool counting) 
     const int64_t nchunks = (h->wd + per - 1) / per;
     const int64_t minband = std::max(K, 8);
     const int64_t waves1 = (rows_total + minband - 1) / minband * nchunks;
-    if (waves1 > 16 * (int64_t)h->cus) return rk;
+    if (waves1 > kSlabMaxWaves1PerCu * (int64_t)h->cus) return rk;
     // K = 16: among the candidate shapes, the least modelled time: a slab is one workgroup per
     // CU, and its time is set by the SIMD with the most rows to update each generation, ceil(W/4)
     // waves x S rows, times the rounds of workgroups over the CUs.  The board decides: 5120^2
@@ -2256,13 +2262,14 @@ int golhip_launch_plan(int64_t width, int64_t height, int strips, int k, int64_t
     const double strip_cells = (double)lcm64(width, 128) * (double)strip_plan_rows(height, strips);
     const int Kfull = pick_k(k);
     // the engine's automatic choice for one strip: the register slab where the streaming kernel
-    // would have at most 16 minimal-band waves per CU (256 CUs), else streaming (pick_reg_kernel)
+    // would have at most kSlabMaxWaves1PerCu minimal-band waves per CU (256 CUs), else streaming
+    // (pick_reg_kernel)
     const int64_t wd = lcm64(width, 128) / 32;
     const int64_t per = golhip::chunk_words(Kfull, golhip::kVariantProd);
     const int64_t waves1 = (height + std::max(Kfull, 8) - 1) / std::max(Kfull, 8) * ((wd + per - 1) / per);
     const bool stream = strips > 1 || !golhip::stencil_slab_supported(Kfull, 8, Kfull == 16 ? 12 : 8,
                                                                        Kfull == 16 ? 9 : 4) ||
-                        waves1 > 16 * 256;
+                        waves1 > kSlabMaxWaves1PerCu * 256;
     LaunchPlanner plan(strip_cells, k, turns, strips == 1 && small_board(cells, Kfull), false, false,
                        4096, stream);
     size_t cnt = 0;

@@ -534,3 +534,25 @@ def test_ring_of_one_equals_single_strip_at_scale(golhip, monkeypatch, width, he
     monkeypatch.delenv("GOLHIP_RING_SELF", raising=False)
     assert np.array_equal(res[True][0], res[False][0])
     assert np.array_equal(res[True][1], res[False][1])
+
+
+@pytest.mark.parametrize("shape", [(12288, 12288, 40), (16384, 8192, 33)])
+def test_mid_board_takes_slab(golhip, oracle, shape):
+    """Mid-size boards (up to kSlabMaxWaves1PerCu minimal-band waves per CU) run the register
+    slab over several rounds of workgroups: the board and every per-turn count against the
+    oracle, with counts (end-of-launch flush) and without."""
+    w, h, turns = shape
+    words = oracle.init_random(w, h, seed=21)
+    with golhip.Engine(w, h, k=16) as e:
+        assert e.launch_kind(16)[0] == "slab" and e.launch_kind(16, counts=True)[0] == "slab"
+        e.load_words(words)
+        counts = e.step(turns, counts=True)
+        got = e.store_words()
+        e.step(turns)
+        got2 = e.store_words()
+    ref = words.copy()
+    ref_counts = oracle.packed_run_words(ref, turns)
+    assert np.array_equal(got, ref)
+    assert np.array_equal(counts.astype(np.int64), ref_counts)
+    oracle.packed_run_words(ref, turns)
+    assert np.array_equal(got2, ref)
