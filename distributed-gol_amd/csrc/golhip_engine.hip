@@ -736,8 +736,10 @@ RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K, bool counting) 
     if (h->force_slab > 0) {  // [NC x 10000 +] W x 100 + S
         const int NC = h->force_slab >= 10000 ? h->force_slab / 10000 : 4;
         const int W = h->force_slab / 100 % 100, S = h->force_slab % 100;
-        if (golhip::stencil_slab_supported(K, W, S, NC))
-            rk.kind = 3, rk.W = W, rk.S = S, rk.NC = NC, rk.T = W * S - 2 * K;
+        // NC = 14 (gol_slabp): P = 64 / (wd + 2) segments of S rows per wave, boards of <= 62 words
+        const int P = NC == 14 ? (h->wd <= 62 ? (int)(64 / (h->wd + 2)) : 0) : 1;
+        if (P > 0 && W * P * S - 2 * K >= 1 && golhip::stencil_slab_supported(K, W, S, NC))
+            rk.kind = 3, rk.W = W, rk.S = S, rk.NC = NC, rk.T = W * P * S - 2 * K;
         return rk;
     }
     if (h->force_tile == 0 || h->force_slab == 0) return rk;

@@ -817,6 +817,167 @@ __global__ __launch_bounds__(64 * W) void gol_slab2(const uint32_t *__restrict__
         }
 }
 
+// gol_slabp: gol_slab2 for NARROW boards (wd <= 30 words: 960 cells or fewer), P = 64 / (wd + 2)
+// sub-chunks packed into each wave.  gol_slab2 gives a wave one chunk of up to 62 words; at wd = 16
+// (configs[0] 512^2) 46 of its 64 lanes carry nothing, and the launch is a chain of barrier-bound
+// generations over a few workgroups (about 1 us per turn whatever the shape, profiles/r04).  Here
+// lane l of a wave is column k = l % L (L = wd + 2: the west halo word, the wd words, the east halo
+// word) of sub-chunk j = l / L, and sub-chunk j holds the wave's S-row segment w * P + j: a
+// workgroup of W waves covers W * P * S rows, P times gol_slab2's, with the same instructions per
+// wave and generation.  The segments' edge rows go through LDS with per-lane addresses (the
+// segment above is the lanes L lower in the same wave, or the previous wave's last sub-chunk), and
+// every count is flushed at the end of the launch (gol_slab2 FM = 2).  Lanes past P * L compute
+// and discard.  The west-only drift of row_sum3 keeps a sub-chunk's garbage west neighbour (the
+// east halo of the sub-chunk before) to its halo lane's low bits, as at lane 0 of gol_slab2.
+template <int K, int W, int S, bool COUNT, int LD>
+__global__ __launch_bounds__(64 * W) void gol_slabp(const uint32_t *__restrict__ in,
+                                                    uint32_t *__restrict__ out, StencilParams p,
+                                                    unsigned long long *__restrict__ slots) {
+    static_assert(K >= 2 && K <= 16 && W >= 1 && S >= 3, "packed slab geometry");
+    __shared__ uint32_t ex[2][W + 2][4][64];  // wave w's block is ex[par][w + 1]; 0 / W + 1 zero
+    __shared__ uint32_t cnt_lds[COUNT ? K : 1][COUNT ? W : 1][64];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int64_t ngroups = p.nbands;  // one chunk (wd <= 30)
+    const int64_t per_xcd = (ngroups + kXcds - 1) / kXcds;
+    const int64_t group = (int64_t)(blockIdx.x % kXcds) * per_xcd + blockIdx.x / kXcds;
+    if (group >= ngroups) return;  // whole workgroup
+    int ya, yb;
+    band_rows(p, group, ya, yb);
+    const int nrows = yb - ya;
+    const int wd = (int)p.wd;
+    const int L = wd + 2, P = 64 / L;
+    const int j = lane / L, k = lane - j * L;
+    const bool live = j < P;
+    const int colraw = k - 1;
+    const int col = (colraw + wd) % wd;
+    const int rowbytes = (int)(p.pitch * 4);
+    const int seg = w * P + j;
+    const int o0 = seg * S - K;  // output row of c[1]
+    uint32_t c[S + 2];
+    c[0] = c[S + 1] = 0;
+    {  // this lane's rows: per-lane row offsets in voffset
+        const int base_row = p.wrap_rows > 0 ? 0 : (int)p.lo;
+        const int span_rows = p.wrap_rows > 0 ? (int)p.wrap_rows : (int)(p.hi - p.lo);
+        const __amdgpu_buffer_rsrc_t irsrc = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint32_t *>(in + (int64_t)base_row * p.pitch), 0, span_rows * rowbytes,
+            kBufferRsrcWord3);
+        RowStream rows(p, ya + o0);
+#pragma unroll
+        for (int r = 0; r < S; ++r) {
+            c[r + 1] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(
+                irsrc, col * 4 + (rows.ly - base_row) * rowbytes, 0, 0);
+            rows.advance();
+        }
+    }
+    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
+        out + (int64_t)ya * p.pitch, 0, nrows * rowbytes, kBufferRsrcWord3);
+    __amdgpu_buffer_rsrc_t drsrc = orsrc;
+    if constexpr (LD == 1)
+        drsrc = __builtin_amdgcn_make_buffer_rsrc(p.diff + (int64_t)ya * p.pitch, 0,
+                                                  nrows * rowbytes, kBufferRsrcWord3);
+    LaneStore ls;
+    if (live && k >= 1 && k <= wd) ls.off_full = col * 4, ls.own_mask = ~0u;
+    const bool count_lane = live && k >= 2 && k <= wd + 1;
+    if constexpr (COUNT)
+        for (int g = 0; g < K; ++g) cnt_lds[g][w][lane] = 0;
+    if (w == 0)
+        for (int par = 0; par < 2; ++par)
+            for (int i = 0; i < 4; ++i) ex[par][0][i][lane] = ex[par][W + 1][i][lane] = 0u;
+    // LDS word offsets within one parity: publish at block w + 1; read the segment above's last row
+    // ([2], [3]) and the segment below's first row ([0], [1])
+    const int pub = (w + 1) * 256 + lane;
+    const int top = j > 0 ? (w + 1) * 256 + 128 + lane - L : w * 256 + 128 + lane + (P - 1) * L;
+    const int bot = j < P - 1 ? (w + 1) * 256 + lane + L : (w + 2) * 256 + lane - (P - 1) * L;
+    constexpr int kExPar = (W + 2) * 4 * 64;
+    uint32_t *const exf = &ex[0][0][0][0];
+    auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    auto gen = [&](auto last_c, int g) {
+        constexpr bool LAST = decltype(last_c)::value;
+        const int gi = g - 1;
+        uint32_t cnt = 0;
+        __amdgpu_buffer_rsrc_t grsrc = orsrc;
+        if constexpr (LD == 2)
+            grsrc = __builtin_amdgcn_make_buffer_rsrc(p.diff + gi * p.diff_stride + (int64_t)ya * p.pitch,
+                                                      0, nrows * rowbytes, kBufferRsrcWord3);
+        auto emit = [&](int r, uint32_t nx, uint32_t centre) {
+            const int o = o0 + r - 1;
+            const bool mine = o >= 0 && o < nrows;  // per lane
+            if (COUNT) cnt = bcnt_acc(mine ? nx : 0u, cnt);
+            if constexpr (LD == 2) {
+                Words<1> dv;
+                dv.w[0] = realign_drift_rt(nx ^ centre, gi);
+                golhip::store_row<1, false>(grsrc, ls, dv, mine ? o * rowbytes : kOutOfRange);
+            }
+            if constexpr (LAST) {
+                const int rowoff = mine ? o * rowbytes : kOutOfRange;
+                Words<1> v;
+                v.w[0] = realign_drift<K>(nx);
+                golhip::store_row<1, false>(orsrc, ls, v, rowoff);
+                if constexpr (LD == 1) {
+                    Words<1> dv;
+                    dv.w[0] = realign_drift<K>(nx ^ centre);
+                    golhip::store_row<1, false>(drsrc, ls, dv, rowoff);
+                }
+            }
+        };
+        uint32_t x[S], s[S], cy[S], ctr[S];
+#pragma unroll
+        for (int i = 0; i < S; ++i) x[i] = c[i + 1];
+        sums_om<S>(x, s, cy, ctr);
+        uint32_t *const e = exf + (g & 1) * kExPar;
+        e[pub] = s[0];
+        e[pub + 64] = cy[0];
+        e[pub + 128] = s[S - 1];
+        e[pub + 192] = cy[S - 1];
+        {
+            constexpr int NI = S - 2;
+            uint32_t as[NI], acy[NI], ms[NI], mcy[NI], mc[NI], bs[NI], bcy[NI], nx[NI];
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                as[i] = s[i], acy[i] = cy[i];
+                ms[i] = s[i + 1], mcy[i] = cy[i + 1], mc[i] = ctr[i + 1];
+                bs[i] = s[i + 2], bcy[i] = cy[i + 2];
+            }
+            life_om<NI>(as, acy, ms, mcy, mc, bs, bcy, nx, AllRows{});
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                emit(i + 2, nx[i], mc[i]);
+                if constexpr (!LAST) c[i + 2] = nx[i];
+            }
+        }
+        lds_barrier();
+        const uint32_t ts = e[top], tcy = e[top + 64];
+        const uint32_t bts = e[bot], btcy = e[bot + 64];
+        {
+            uint32_t as[2] = {ts, s[S - 2]}, acy[2] = {tcy, cy[S - 2]};
+            uint32_t ms[2] = {s[0], s[S - 1]}, mcy[2] = {cy[0], cy[S - 1]}, mc[2] = {ctr[0], ctr[S - 1]};
+            uint32_t bs[2] = {s[1], bts}, bcy[2] = {cy[1], btcy}, nx[2];
+            life_om<2>(as, acy, ms, mcy, mc, bs, bcy, nx, AllRows{});
+            emit(1, nx[0], mc[0]);
+            emit(S, nx[1], mc[1]);
+            if constexpr (!LAST) {
+                c[1] = nx[0];
+                c[S] = nx[1];
+            }
+        }
+        if constexpr (COUNT) cnt_lds[gi][w][lane] = cnt;
+    };
+#pragma clang loop unroll(disable)
+    for (int g = 1; g < K; ++g) gen(std::false_type{}, g);
+    gen(std::true_type{}, K);
+    if constexpr (COUNT) {
+        lds_barrier();
+        for (int g = w; g < K; g += W) {
+            uint32_t a = 0;
+#pragma unroll
+            for (int ww = 0; ww < W; ++ww) a += cnt_lds[g][ww][lane];
+            uint32_t acc[1] = {count_lane ? a : 0u};
+            flush_counts<1>(acc, g, lane, group, slots);
+        }
+    }
+}
+
 // gol_slab3: gol_slab2 software-pipelined across generations.  The phase stamps of gol_slab2
 // (profiles/r04/r04n_slab_stamps.log: configs[1] 5120^2 with every count, 14.4 us per 16-turn
 // launch, 10.5 of them in the generation loop, 0.66 us per generation for ~0.4 us of VALU issue)
@@ -1096,6 +1257,7 @@ constexpr int kSlab3 = 10;  // gol_slab3: gol_slab2 pipelined across generations
 constexpr int kSlab2F = 11;  // gol_slab2, counts flushed in the launch whenever S <= K (FM = 1)
 constexpr int kSlab2E = 12;  // gol_slab2, counts flushed at the end of the launch (FM = 2)
 constexpr int kSlab2P = 13;  // gol_slab2 FM = 2 with the younger half of the waves at s_setprio 1
+constexpr int kSlabP = 14;  // gol_slabp: P = 64 / (wd + 2) row segments packed per wave (wd <= 62)
 constexpr bool slab_prod_ws(int K, int W, int S) {
     return (K == 16 && W == 8 && S == 12) || (K == 16 && W == 12 && S == 8) ||
            (K == 16 && W == 12 && S == 7) || (K == 16 && W == 16 && S == 6) || (K == 8 && W == 8 && S == 8) ||
@@ -1134,6 +1296,30 @@ hipError_t launch_slab_kws(const uint32_t *in, uint32_t *out, const StencilParam
             hipLaunchKernelGGL((gol_slab3<K, W, S, true, 0>), dim3(blocks), block, 0, s, in, out, p, slots);
         else
             hipLaunchKernelGGL((gol_slab3<K, W, S, false, 0>), dim3(blocks), block, 0, s, in, out, p, slots);
+        return hipGetLastError();
+    }
+    if constexpr (NC == kSlabP) {
+        if (p.wd > 62 || p.nchunks != 1) return hipErrorInvalidValue;
+        if (p.diff && p.diff_stride > 0) {
+            if constexpr (slab_prod_shape(K, W, S, NC)) {
+                if (slots)
+                    hipLaunchKernelGGL((gol_slabp<K, W, S, true, 2>), dim3(blocks), block, 0, s, in, out, p, slots);
+                else
+                    hipLaunchKernelGGL((gol_slabp<K, W, S, false, 2>), dim3(blocks), block, 0, s, in, out, p, slots);
+                return hipGetLastError();
+            } else {
+                return hipErrorNotSupported;
+            }
+        }
+        const int ld = p.diff ? 1 : 0;
+        if (ld && slots)
+            hipLaunchKernelGGL((gol_slabp<K, W, S, true, 1>), dim3(blocks), block, 0, s, in, out, p, slots);
+        else if (ld)
+            hipLaunchKernelGGL((gol_slabp<K, W, S, false, 1>), dim3(blocks), block, 0, s, in, out, p, slots);
+        else if (slots)
+            hipLaunchKernelGGL((gol_slabp<K, W, S, true, 0>), dim3(blocks), block, 0, s, in, out, p, slots);
+        else
+            hipLaunchKernelGGL((gol_slabp<K, W, S, false, 0>), dim3(blocks), block, 0, s, in, out, p, slots);
         return hipGetLastError();
     }
     if constexpr (NC == kSlab2F || NC == kSlab2E || NC == kSlab2P) {
@@ -1184,26 +1370,28 @@ hipError_t launch_slab_kws(const uint32_t *in, uint32_t *out, const StencilParam
             hipLaunchKernelGGL((gol_slab2<K, W, S, false, 0>), dim3(blocks), block, 0, s, in, out, p, slots);
         return hipGetLastError();
     }
-    if (p.diff && p.diff_stride > 0) {
-        if constexpr (slab_prod_shape(K, W, S, NC)) {
-            if (slots)
-                hipLaunchKernelGGL((gol_slab<K, W, S, true, 2, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
-            else
-                hipLaunchKernelGGL((gol_slab<K, W, S, false, 2, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
-            return hipGetLastError();
-        } else {
-            return hipErrorNotSupported;
+    if constexpr (NC != kSlabP) {
+        if (p.diff && p.diff_stride > 0) {
+            if constexpr (slab_prod_shape(K, W, S, NC)) {
+                if (slots)
+                    hipLaunchKernelGGL((gol_slab<K, W, S, true, 2, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
+                else
+                    hipLaunchKernelGGL((gol_slab<K, W, S, false, 2, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
+                return hipGetLastError();
+            } else {
+                return hipErrorNotSupported;
+            }
         }
-    }
-    if (p.diff) {
-        if (slots)
-            hipLaunchKernelGGL((gol_slab<K, W, S, true, 1, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
-        else
-            hipLaunchKernelGGL((gol_slab<K, W, S, false, 1, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
-    } else if (slots) {
-        hipLaunchKernelGGL((gol_slab<K, W, S, true, 0, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
-    } else {
-        hipLaunchKernelGGL((gol_slab<K, W, S, false, 0, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
+        if (p.diff) {
+            if (slots)
+                hipLaunchKernelGGL((gol_slab<K, W, S, true, 1, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
+            else
+                hipLaunchKernelGGL((gol_slab<K, W, S, false, 1, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
+        } else if (slots) {
+            hipLaunchKernelGGL((gol_slab<K, W, S, true, 0, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
+        } else {
+            hipLaunchKernelGGL((gol_slab<K, W, S, false, 0, NC>), dim3(blocks), block, 0, s, in, out, p, slots);
+        }
     }
     return hipGetLastError();
 }
@@ -1228,7 +1416,10 @@ hipError_t launch_slab_kws(const uint32_t *in, uint32_t *out, const StencilParam
     X(8, 8, 8, 9) X(12, 8, 8, 9) X(16, 16, 5, 9) X(16, 10, 8, 9) X(16, 8, 8, 9) X(16, 12, 6, 9) \
     X(16, 8, 12, 10) X(16, 16, 6, 10) X(16, 12, 8, 10) X(16, 12, 7, 10) X(16, 10, 8, 10) X(16, 8, 10, 10) \
     X(16, 8, 12, 11) X(16, 8, 10, 11) X(16, 10, 8, 11) X(16, 12, 8, 11) \
-    X(16, 16, 5, 12) X(16, 16, 6, 13) X(16, 12, 7, 13) X(16, 8, 12, 13)
+    X(16, 16, 5, 12) X(16, 16, 6, 13) X(16, 12, 7, 13) X(16, 8, 12, 13) \
+    X(16, 4, 3, 14) X(16, 4, 4, 14) X(16, 8, 3, 14) X(16, 8, 4, 14) X(16, 8, 6, 14) X(16, 16, 3, 14) \
+    X(16, 4, 5, 14) X(16, 4, 6, 14) X(16, 6, 3, 14) X(16, 12, 3, 14) X(16, 2, 6, 14) X(16, 2, 8, 14) \
+    X(12, 8, 3, 14) X(12, 4, 3, 14) X(8, 8, 3, 14) X(8, 4, 3, 14) X(8, 4, 4, 14)
 #define GOLHIP_TILE_CONFIGS(X) \
     X(2, 16) X(4, 8) X(4, 16) X(4, 32) X(6, 16) X(8, 8) X(8, 16) X(8, 32) X(10, 16) X(12, 8) \
     X(12, 16) X(12, 32) X(14, 16) X(16, 8) X(16, 16) X(16, 32)

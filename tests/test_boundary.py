@@ -153,8 +153,12 @@ def test_launch_plan_bulk_depth_by_board_size(golhip):
     # the driver's 20-turn region stays 12 + 8 (a 6-deep launch runs at ~3/4 the rate)
     assert sorted(golhip.launch_plan(65536, 65536, 16, 20)) == [8, 12]
     assert sorted(golhip.launch_plan(65536, 131072, 16, 20, strips=2)) == [8, 12]
+    # 16384^2 takes the register slab since round 4 (at most 40 minimal-band waves per CU): 8
+    # launches of K = 16 per replay; 20480^2 still streams: 10 launches of K = 12 per replay
     graphs16k = [-d for d in golhip.launch_plan(16384, 16384, 16, 2000) if d < 0]
-    assert graphs16k and set(graphs16k) == {120}  # 10 launches of K = 12 per replay
+    assert graphs16k and set(graphs16k) == {128}
+    graphs20k = [-d for d in golhip.launch_plan(20480, 20480, 16, 2000) if d < 0]
+    assert graphs20k and set(graphs20k) == {120}
     graphs5k = [-d for d in golhip.launch_plan(5120, 5120, 16, 10000) if d < 0]
     assert graphs5k[:2] == [4096, 4096]  # the register slab keeps K = 16
     # the maximum depth still caps everything

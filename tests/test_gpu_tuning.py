@@ -5,6 +5,8 @@ slab shapes the planner does not pick, selected by the tuning build's environmen
 The production library (lib/libgolhip.so) contains none of these kernels and reads none of these
 variables (tests/test_boundary.py checks its strings); tests/test_gpu_parity.py covers it.
 """
+import math
+
 import numpy as np
 import pytest
 
@@ -235,3 +237,44 @@ def test_slab2_flips_ring_every_turn(golhip, tuning, oracle, monkeypatch, code, 
                 assert int(alive[t]) == int((cur == 255).sum())
                 prev = cur
         assert np.array_equal(e.store(), prev)
+
+
+PACKED_CONFIGS = [140403, 140404, 140803, 140804, 140806, 141603]
+
+
+@pytest.mark.parametrize("code", PACKED_CONFIGS)
+def test_packed_slab_kernel(golhip, tuning, oracle, monkeypatch, code):
+    """gol_slabp (NC = 14): P = 64 / (wd + 2) row segments packed into each wave, for boards of at
+    most 62 packed words (1984 cells); P = 10 at 16..128 cells wide, 3 at 512, 1 at 1920 / 1984:
+    wrap, short boards, boards shorter than a workgroup, ragged widths, per-turn counts, and the
+    last generation's flips (LD = 1)."""
+    monkeypatch.setenv("GOLHIP_SLAB", str(code))
+    k = 16
+    for (h, w) in [(512, 512), (16, 16), (77, 640), (5, 96), (300, 64), (1000, 128), (33, 256),
+                   (129, 960), (250, 1984), (40, 1000), (700, 512)]:
+        rng = np.random.default_rng(h * 7 + w + code)
+        board = ((rng.random((h, w)) < 0.4) * 255).astype(np.uint8)
+        turns = 3 * k + 1
+        exp, exp_counts = oracle.packed_run(board, turns)
+        wd = math.lcm(w, 128) // 32
+        waves, rows = code // 100 % 100, code % 100
+        packed = waves * (64 // (wd + 2)) * rows - 2 * k >= 1  # else the engine streams
+        with golhip.Engine(w, h, k=k, lib=tuning) as e:
+            assert (e.launch_kind(k) == ("slab", code)) == packed, (h, w)
+        out, counts, _, _ = run_engine(golhip, board, turns, k=k, counts=True, lib=tuning)
+        assert np.array_equal(out, exp), (code, h, w)
+        assert np.array_equal(counts.astype(np.int64), exp_counts), (code, h, w)
+    h, w = 300, 512
+    rng = np.random.default_rng(code)
+    board = ((rng.random((h, w)) < 0.4) * 255).astype(np.uint8)
+    before, _ = oracle.packed_run(board, 2 * k - 1)
+    exp, _ = oracle.packed_run(board, 2 * k)
+    with golhip.Engine(w, h, k=k, lib=tuning) as e:
+        e.set_fixed_k(True)
+        e.track_flips(True)
+        e.load(board)
+        e.step(2 * k)
+        assert e.launch_kind(k) == ("slab", code)
+        got = [tuple(c) for c in e.flips().tolist()]
+        assert np.array_equal(e.store(), exp)
+    assert got == oracle.flips(before, exp)
