@@ -773,6 +773,23 @@ RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K, bool counting) 
     // best at 5120^2 with and without counts once the counting loop lost its add3 tree and the
     // exchange its branches (0.916 vs 0.931 us/turn for 12 x 8 with every count, 0.806 vs 0.828
     // without: profiles/r03/r03k_tune_slab.log).
+    // Narrow boards (wd <= 30 packed words, P = 64 / (wd + 2) >= 2 row segments per wave: the
+    // reference's test sizes up to 512 and configs[0]) take the packed slab gol_slabp (NC = 14):
+    // the launch is a chain of barrier-bound generations, fastest with few waves per workgroup --
+    // the first of 4 / 6 / 8 waves x 3 rows whose workgroups fit one round over the CUs, else 8 x 3
+    // (1600 turns, every count: 512^2 4 x 3 0.570 us/turn vs 0.811 for gol_slab2 12 x 7; 4096 x 512
+    // 6 x 3 0.598 (4 x 3 with 1024 workgroups 0.806); 640^2 (P = 2) 6 x 3 0.604 / 8 x 3 0.590 vs
+    // 0.809; without counts 0.37 - 0.42 vs 0.70: profiles/r04/r04p4_narrow_sweep.log, r04p5)
+    if (K == 16 && h->wd <= 30) {
+        const int P = (int)(64 / (h->wd + 2));
+        for (const int W : {4, 6, 8}) {
+            const int T = W * P * 3 - 2 * K;
+            if (T < 1 || !golhip::stencil_slab_supported(K, W, 3, 14)) continue;
+            rk.kind = 3, rk.W = W, rk.S = 3, rk.NC = 14, rk.T = T;
+            if ((rows_total + T - 1) / T <= h->cus) break;
+        }
+        if (rk.kind) return rk;
+    }
     struct Cand {
         int W, S, NC;
     };

@@ -1261,11 +1261,11 @@ constexpr int kSlabP = 14;  // gol_slabp: P = 64 / (wd + 2) row segments packed 
 constexpr bool slab_prod_ws(int K, int W, int S) {
     return (K == 16 && W == 8 && S == 12) || (K == 16 && W == 12 && S == 8) ||
            (K == 16 && W == 12 && S == 7) || (K == 16 && W == 16 && S == 6) || (K == 8 && W == 8 && S == 8) ||
-           (K == 12 && W == 8 && S == 8);
+           (K == 12 && W == 8 && S == 8) || (K == 16 && S == 3 && (W == 4 || W == 6 || W == 8));
 }
 constexpr bool slab_prod_shape(int K, int W, int S, int NC) {
     return slab_prod_ws(K, W, S) &&
-           (NC == kSlab2 || NC == kSlab3 || NC == kSlab2F || NC == kSlab2E || NC == kSlab2P ||
+           (NC == kSlab2 || NC == kSlab3 || NC == kSlab2F || NC == kSlab2E || NC == kSlab2P || NC == kSlabP ||
             (K == 16 ? NC == 2 : NC == 4));
 }
 
@@ -1404,10 +1404,12 @@ hipError_t launch_slab_kws(const uint32_t *in, uint32_t *out, const StencilParam
 // Round 4: K = 16 runs gol_slab2 (NC = 9) in production (configs[1] 5120^2 with every count 0.908
 // -> 0.843 us/turn, configs[4]-sized 4096^2 0.829 -> 0.781; profiles/r04/r04c_tune_slab.log), and
 // with counts gol_slab2 flushing every generation's count at the end of the launch (NC = 12: 0.772
-// at 5120^2 with 16 x 6, 0.730 at 4096^2 with 12 x 7; profiles/r04/r04u_tune.log).
+// at 5120^2 with 16 x 6, 0.730 at 4096^2 with 12 x 7; profiles/r04/r04u_tune.log).  Narrow boards
+// (wd <= 30) run the packed gol_slabp (NC = 14) at 4 / 6 / 8 waves x 3 rows (512^2 with every
+// count 0.811 -> 0.570 us/turn, without 0.708 -> 0.373: profiles/r04/r04p4_narrow_sweep.log).
 #define GOLHIP_SLAB_PROD_CONFIGS(X) \
     X(8, 8, 8, 4) X(12, 8, 8, 4) X(16, 8, 12, 9) X(16, 16, 6, 9) X(16, 12, 8, 9) X(16, 12, 7, 9) \
-    X(16, 16, 6, 12) X(16, 12, 7, 12) X(16, 12, 8, 12)
+    X(16, 16, 6, 12) X(16, 12, 7, 12) X(16, 12, 8, 12) X(16, 4, 3, 14) X(16, 6, 3, 14) X(16, 8, 3, 14)
 #ifdef GOLHIP_TUNING
 #define GOLHIP_SLAB_CONFIGS(X) GOLHIP_SLAB_PROD_CONFIGS(X) \
     X(16, 8, 12, 2) X(16, 12, 8, 2) X(16, 12, 7, 2) \
@@ -1417,8 +1419,8 @@ hipError_t launch_slab_kws(const uint32_t *in, uint32_t *out, const StencilParam
     X(16, 8, 12, 10) X(16, 16, 6, 10) X(16, 12, 8, 10) X(16, 12, 7, 10) X(16, 10, 8, 10) X(16, 8, 10, 10) \
     X(16, 8, 12, 11) X(16, 8, 10, 11) X(16, 10, 8, 11) X(16, 12, 8, 11) \
     X(16, 16, 5, 12) X(16, 16, 6, 13) X(16, 12, 7, 13) X(16, 8, 12, 13) \
-    X(16, 4, 3, 14) X(16, 4, 4, 14) X(16, 8, 3, 14) X(16, 8, 4, 14) X(16, 8, 6, 14) X(16, 16, 3, 14) \
-    X(16, 4, 5, 14) X(16, 4, 6, 14) X(16, 6, 3, 14) X(16, 12, 3, 14) X(16, 2, 6, 14) X(16, 2, 8, 14) \
+    X(16, 4, 4, 14) X(16, 8, 4, 14) X(16, 8, 6, 14) X(16, 16, 3, 14) \
+    X(16, 4, 5, 14) X(16, 4, 6, 14) X(16, 12, 3, 14) X(16, 2, 6, 14) X(16, 2, 8, 14) \
     X(12, 8, 3, 14) X(12, 4, 3, 14) X(8, 8, 3, 14) X(8, 4, 3, 14) X(8, 4, 4, 14)
 #define GOLHIP_TILE_CONFIGS(X) \
     X(2, 16) X(4, 8) X(4, 16) X(4, 32) X(6, 16) X(8, 8) X(8, 16) X(8, 32) X(10, 16) X(12, 8) \

@@ -556,3 +556,31 @@ def test_mid_board_takes_slab(golhip, oracle, shape):
     assert np.array_equal(counts.astype(np.int64), ref_counts)
     oracle.packed_run_words(ref, turns)
     assert np.array_equal(got2, ref)
+
+
+@pytest.mark.parametrize("shape,code", [((512, 512), 140403), ((512, 4096), 140603), ((640, 640), 140603),
+                                        ((256, 16384), 140603), ((128, 2048), 140403), ((64, 64), 140403),
+                                        ((384, 384), 140403), ((896, 200), 140603), ((512, 100000), 140803)])
+def test_narrow_board_takes_packed_slab(golhip, oracle, shape, code):
+    """Narrow boards (at most 30 packed words) run the packed register slab gol_slabp (NC = 14, P =
+    64 / (wd + 2) row segments per wave) at the first of 4 / 6 / 8 waves x 3 rows whose workgroups
+    fit one round over the CUs: the board and every per-turn count against the oracle, with counts
+    and without (the tall 100000-row board only the shape choice)."""
+    w, h = shape
+    with golhip.Engine(w, h, k=16) as e:
+        assert e.launch_kind(16) == ("slab", code)
+        assert e.launch_kind(16, counts=True) == ("slab", code)
+        if h > 20000:
+            return
+        words = oracle.init_random(w, h, seed=23)
+        e.load_words(words)
+        counts = e.step(2 * 16 + 5, counts=True)
+        got = e.store_words()
+        e.step(48)
+        got2 = e.store_words()
+    ref = words.copy()
+    ref_counts = oracle.packed_run_words(ref, 2 * 16 + 5)
+    assert np.array_equal(got, ref)
+    assert np.array_equal(counts.astype(np.int64), ref_counts)
+    oracle.packed_run_words(ref, 48)
+    assert np.array_equal(got2, ref)
