@@ -45,6 +45,7 @@ constexpr bool kTuningBuildEngine = golhip::kTuningBuild;
 // without counts (12288^2 2.82 vs 3.14 us/turn, 16384^2 4.09 vs 4.40), even at 20480^2, and
 // slower there with counts (9.33 vs 8.39); 16384^2 has 36 such waves per CU, 20480^2 55.
 constexpr int64_t kSlabMaxWaves1PerCu = 40;
+constexpr int64_t kPinnedCountTurns = 4096;  // calls up to this many turns return counts pinned
 constexpr int64_t kStampWaves = 1 << 20;  // tuning build: waves of the per-wave stamp buffer
 // Default deadline of a host wait on RCCL-dependent work and of the communicator's set-up
 // (golhip_set_comm_timeout(NULL, ms) changes it for later creates): well under the 600 s a driver
@@ -66,8 +67,14 @@ struct Shard {
     uint32_t *buf[2] = {nullptr, nullptr};  // allocation base (halo rows first)
     unsigned long long *slots = nullptr;    // count_window x kCountSlots
     unsigned long long *scratch_u64 = nullptr;
-    unsigned long long *d_counts = nullptr;
-    size_t d_counts_cap = 0;
+    // the call's per-turn counts: dev_counts, or on a one-shard engine without RCCL for calls of
+    // at most kPinnedCountTurns turns pin_counts (pinned host memory, hipHostMalloc coherent): the
+    // count finalize writes it directly and the call returns without a device-to-host copy
+    // (configs[0], 100 turns: the copy and its dispatch gap were ~17 of ~85 us per call)
+    unsigned long long *d_counts = nullptr;  // = dev_counts or pin_counts for this call
+    bool counts_host = false;
+    unsigned long long *dev_counts = nullptr, *pin_counts = nullptr;
+    size_t dev_counts_cap = 0, pin_counts_cap = 0;
     ncclComm_t comm_nccl = nullptr;
     // flips (gol/distributor.go:53-59): the last generation's flips board (golhip_track_flips)
     // and a ring of one flips board per turn (golhip_step_flips), rows x pitch words each
@@ -431,7 +438,8 @@ void free_shard(Shard &s, int64_t drain_ms = 0, bool comm_failed = false) {
         if (b) (void)hipFree(b);
     if (s.slots) (void)hipFree(s.slots);
     if (s.scratch_u64) (void)hipFree(s.scratch_u64);
-    if (s.d_counts) (void)hipFree(s.d_counts);
+    if (s.dev_counts) (void)hipFree(s.dev_counts);
+    if (s.pin_counts) (void)hipHostFree(s.pin_counts);
     for (void *q : {(void *)s.diffbuf, (void *)s.ring, (void *)s.ex_rowcounts, (void *)s.ex_offsets,
                     (void *)s.ex_slot_counts, (void *)s.ex_xy, (void *)s.stage,
                     (void *)s.ex_block_sums})
@@ -1206,6 +1214,15 @@ int reduce_u64(golhip_t h, const std::vector<unsigned long long *> &bufs, size_t
         int rc = comm_ready(h, s.comm_nccl, "the count all-reduce");
         if (rc) return rc;
     }
+    if (h->shards.size() == 1 && h->shards[0].counts_host && bufs[0] == h->shards[0].d_counts) {
+        Shard &s = h->shards[0];  // pinned: written by the finalize kernels in stream order
+        HIPCHK(h, hipSetDevice(s.device));
+        SYNCCHK(h, s.compute);
+        std::memcpy(out, bufs[0], n * sizeof(uint64_t));
+        if (h->host_comm_on && h->split && h->host_comm.allreduce_u64(h->host_comm.ctx, out, n) != 0)
+            return fail(h, GOLHIP_ERR_RCCL, "host transport: all-reduce of %zu counts failed", n);
+        return GOLHIP_OK;
+    }
     std::vector<uint64_t> tmp(n);
     for (size_t i = 0; i < h->shards.size(); ++i) {
         Shard &s = h->shards[i];
@@ -1830,15 +1847,27 @@ static int run_steps(golhip_t h, int64_t turns, uint64_t *alive_per_turn, bool r
                     h->variant);
     const bool counting = alive_per_turn != nullptr;
     if (counting) {
+        // long calls keep the device buffer: their graph replays copy each replay's counts into it
+        // (device to device) and one copy returns them
+        const bool host_counts = h->shards.size() == 1 && !rccl_waits(h) && turns <= kPinnedCountTurns;
         for (auto &s : h->shards) {
-            if (s.d_counts_cap < (size_t)turns) {
+            unsigned long long *&buf = host_counts ? s.pin_counts : s.dev_counts;
+            size_t &cap = host_counts ? s.pin_counts_cap : s.dev_counts_cap;
+            if (cap < (size_t)turns) {
                 HIPCHK(h, hipSetDevice(s.device));
                 SYNCCHK(h, s.compute);
-                if (s.d_counts) HIPCHK(h, hipFree(s.d_counts));
-                s.d_counts = nullptr;
-                HIPCHK(h, hipMalloc(&s.d_counts, sizeof(unsigned long long) * (size_t)turns));
-                s.d_counts_cap = (size_t)turns;
+                if (buf) HIPCHK(h, host_counts ? hipHostFree(buf) : hipFree(buf));
+                buf = nullptr;
+                cap = 0;
+                const size_t n = (size_t)std::max<int64_t>(turns, 128);
+                if (host_counts)
+                    HIPCHK(h, hipHostMalloc((void **)&buf, n * sizeof(unsigned long long), hipHostMallocCoherent));
+                else
+                    HIPCHK(h, hipMalloc(&buf, n * sizeof(unsigned long long)));
+                cap = n;
             }
+            s.d_counts = buf;
+            s.counts_host = host_counts;
         }
     }
     // Timing: ONE event pair around the whole call on the first strip's compute stream (per-
@@ -1878,7 +1907,8 @@ static int run_steps(golhip_t h, int64_t turns, uint64_t *alive_per_turn, bool r
             if (counting)
                 HIPCHK(h, hipMemcpyAsync(s.d_counts + done, h->g_counts,
                                          sizeof(unsigned long long) * (size_t)M * Kfull,
-                                         hipMemcpyDeviceToDevice, s.compute));
+                                         s.counts_host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice,
+                                         s.compute));
             done += (int64_t)M * Kfull;
             h->turn += (int64_t)M * Kfull;
             h->prev_valid = (Kfull == 1);
