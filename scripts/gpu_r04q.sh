@@ -1,14 +1,14 @@
 #!/bin/bash
-# round 4 (q): the packed narrow-board slab in production: GPU suite, smoke, default bench line
+# round 4 (q): the 20-turn ring of one and the single strip, last dispatches raw (where the
+# ring's extra ~40 us of kernel span go)
 set -u
 O=gpurun_out/r04q
 mkdir -p $O
 export TMPDIR=/tmp
 G=scripts/guard.sh
-$G 900 $O/suite.log python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread || exit $?
-tail -3 $O/suite.log
-grep -q " passed" $O/suite.log && ! grep -q "failed" $O/suite.log || exit 1
-$G 200 $O/smoke.log python3 -c "import __graft_entry__ as g; g.smoke()" || exit $?
-tail -2 $O/smoke.log
-$G 400 $O/bench.log python3 bench.py || exit $?
-grep '^{' $O/bench.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["roofline"]["frac"], d["parity"]["ok"], d["parity"].get("digest_ok")); print(json.dumps(d.get("configs")))'
+for ring in 1 0; do
+  $G 200 $O/run20_ring$ring.log rocprofv3 --kernel-trace --output-format csv -d /tmp/r04q_$ring -o t -- python3 scripts/ring_timeline.py run 65536 20 $ring 5 || exit $?
+  grep "^{" $O/run20_ring$ring.log
+  python3 scripts/ring_timeline.py /tmp/r04q_$ring tail 14 > $O/tail20_ring$ring.txt 2>&1
+  cat $O/tail20_ring$ring.txt
+done

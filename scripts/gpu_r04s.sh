@@ -1,17 +1,13 @@
 #!/bin/bash
-# round 4 (s): per-turn counts through a pinned host buffer (no device-to-host copy per call):
-# configs[0] call time, GPU suite, smoke, default bench line
+# round 4 (s): tuning-build launch depths 20 / 24 -- parity, then the driver's 20-turn region as ONE
+# K = 20 launch against 12 + 8 (density-matched lockstep A/B), and the 1000-turn rate at K = 20
 set -u
 O=gpurun_out/r04s
 mkdir -p $O
 export TMPDIR=/tmp
 G=scripts/guard.sh
-$G 120 $O/cfg0.log python3 -u scripts/trace_cfg0.py || exit $?
-cat $O/cfg0.log
-$G 900 $O/suite.log python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread || exit $?
-tail -3 $O/suite.log
-grep -q " passed" $O/suite.log && ! grep -q "failed" $O/suite.log || exit 1
-$G 200 $O/smoke.log python3 -c "import __graft_entry__ as g; g.smoke()" || exit $?
-tail -2 $O/smoke.log
-$G 400 $O/bench.log python3 bench.py || exit $?
-grep '^{' $O/bench.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["roofline"]["frac"], d["parity"]["ok"], d["parity"].get("digest_ok")); print(json.dumps(d.get("configs")))'
+$G 300 $O/parity.log python -u -m pytest tests/test_gpu_tuning.py -m gpu -x -q -k "depths_20_24" --timeout 240 --timeout-method thread || exit $?
+tail -2 $O/parity.log
+grep -q " passed" $O/parity.log && ! grep -qE " failed| error" $O/parity.log || exit 1
+$G 300 $O/ab_split.log python3 scripts/ab_split.py prod 0,12,20,16 11 || exit $?
+tail -6 $O/ab_split.log
