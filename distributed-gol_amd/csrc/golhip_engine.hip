@@ -45,7 +45,10 @@ constexpr bool kTuningBuildEngine = golhip::kTuningBuild;
 // without counts (12288^2 2.82 vs 3.14 us/turn, 16384^2 4.09 vs 4.40), even at 20480^2, and
 // slower there with counts (9.33 vs 8.39); 16384^2 has 36 such waves per CU, 20480^2 55.
 constexpr int64_t kSlabMaxWaves1PerCu = 40;
-constexpr int64_t kPinnedCountTurns = 4096;  // calls up to this many turns return counts pinned
+// calls up to this many turns return their counts pinned: shorter than the planner's smallest
+// replayed graph (128 generations), whose per-replay count copy into pinned memory cost more than
+// the one device-to-host copy it saves (1600 turns at 512^2: 0.570 -> 0.705 us/turn with 4096)
+constexpr int64_t kPinnedCountTurns = 127;
 constexpr int64_t kStampWaves = 1 << 20;  // tuning build: waves of the per-wave stamp buffer
 // Default deadline of a host wait on RCCL-dependent work and of the communicator's set-up
 // (golhip_set_comm_timeout(NULL, ms) changes it for later creates): well under the 600 s a driver
@@ -68,7 +71,7 @@ struct Shard {
     unsigned long long *slots = nullptr;    // count_window x kCountSlots
     unsigned long long *scratch_u64 = nullptr;
     // the call's per-turn counts: dev_counts, or on a one-shard engine without RCCL for calls of
-    // at most kPinnedCountTurns turns pin_counts (pinned host memory, hipHostMalloc coherent): the
+    // at most kPinnedCountTurns (127) turns pin_counts (pinned host memory, hipHostMalloc coherent): the
     // count finalize writes it directly and the call returns without a device-to-host copy
     // (configs[0], 100 turns: the copy and its dispatch gap were ~17 of ~85 us per call)
     unsigned long long *d_counts = nullptr;  // = dev_counts or pin_counts for this call

@@ -587,14 +587,14 @@ def test_narrow_board_takes_packed_slab(golhip, oracle, shape, code):
 
 
 def test_counts_pinned_and_device_buffers_interleaved(golhip, oracle):
-    """Calls of at most 4096 turns return their per-turn counts through pinned host memory, longer
+    """Calls of at most 127 turns return their per-turn counts through pinned host memory, longer
     calls through the device buffer (graph replays): interleaved on one engine, every count and
     the board against the oracle."""
     words = oracle.init_random(512, 512, seed=31)
     ref = words.copy()
     with golhip.Engine(512, 512, k=16) as e:
         e.load_words(words)
-        for turns in (100, 5000, 37, 4096, 1):
+        for turns in (100, 5000, 37, 127, 128, 4096, 1):
             counts = e.step(turns, counts=True)
             assert np.array_equal(counts.astype(np.int64), oracle.packed_run_words(ref, turns)), turns
         assert np.array_equal(e.store_words(), ref)
