@@ -173,16 +173,17 @@ class ShmBarrier:
         self.path, self.mm, self.fd = path, mm, fd
 
     @classmethod
-    def create(cls, rank: int, world: int, timeout_s: float) -> "ShmBarrier | None":
-        """Collective: every rank maps the page, or every rank gets None (a rank that cannot create
-        or map it -- no /dev/shm, a full one -- and the others then keep the process group's barrier
-        too, so the ranks never disagree on which barrier they wait in)."""
+    def create(cls, rank: int, world: int, timeout_s: float, local_ok: bool = True) -> "ShmBarrier | None":
+        """Collective (every rank calls it): every rank maps the page, or every rank gets None.  A
+        rank whose own checks fail (local_ok False: not every rank on this node, no /dev/shm) or
+        that cannot create or map the page votes no, and then every rank keeps the process group's
+        barrier, so the ranks never disagree on which barrier they wait in."""
         import mmap
         name = [f"/dev/shm/golhip_bench_{os.getpid()}_{time.time_ns()}" if rank == 0 else None]
         if world > 1:
             dist.broadcast_object_list(name, src=0)
-        path, size, ok, mm, fd = name[0], 64 * world, True, None, -1
-        if rank == 0:
+        path, size, ok, mm, fd = name[0], 64 * world, bool(local_ok), None, -1
+        if rank == 0 and ok:
             try:
                 with open(path, "wb") as f:
                     f.write(b"\0" * size)
@@ -190,11 +191,12 @@ class ShmBarrier:
                 ok = False
         if world > 1:
             barrier()
-        try:
-            fd = os.open(path, os.O_RDWR)
-            mm = mmap.mmap(fd, size)
-        except (OSError, ValueError):
-            ok = False
+        if ok:
+            try:
+                fd = os.open(path, os.O_RDWR)
+                mm = mmap.mmap(fd, size)
+            except (OSError, ValueError):
+                ok = False
         oks = [ok]
         if world > 1:
             oks = [None] * world
@@ -242,7 +244,13 @@ def barrier():
         dist.barrier()
 
 
+RANK_TIMES: list = []  # every rank's seconds of the last timed_steps region (rank order)
+
+
 def timed_steps(eng: golhip.Engine, steps: int, world: int) -> float:
+    """Seconds of `steps` generations between barriers, the max over the ranks (RANK_TIMES keeps
+    every rank's own)."""
+    global RANK_TIMES
     if dist.is_initialized():  # N > 1, or the --pg-always rehearsal
         barrier()
     torch.cuda.synchronize()
@@ -258,11 +266,14 @@ def timed_steps(eng: golhip.Engine, steps: int, world: int) -> float:
         barrier()
     dt = time.perf_counter() - t0
     eng.sync()
+    RANK_TIMES = [dt]
     if dist.is_initialized():
-        t = torch.tensor([dt], dtype=torch.float64,
-                         device="cuda" if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        parts = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+        dist.all_gather(parts, t)
+        RANK_TIMES = [float(x.item()) for x in parts]
+        dt = max(RANK_TIMES)
     return dt
 
 
@@ -350,8 +361,16 @@ def cpu_baseline(size: int, turns: int, threads_per_server: int | None = None) -
                          "cfg2_gcups": round(5120 * 5120 * 20 / dt2 / 1e9, 4),
                          "cfg2_counts_match": [int(x) for x in c2] == want2}
     del b2
+    # the job's CPUs: its affinity set and its cgroup quota, whichever is smaller (the GPU box
+    # shares its host; os.cpu_count() shows the whole machine)
+    effective = min(x for x in (share.get("affinity_cpus") or nproc, quota or nproc, nproc) if x)
+    effective = max(1, int(effective))
     best_t = max(sweep, key=lambda t: sweep[t]["cfg2_gcups"])
-    T = threads_per_server or int(best_t)
+    # the value's T: the fastest of the sweep among those whose 4T threads fit the job's CPUs
+    # (oversubscribing the quota measures the scheduler, and would make `cores` exceed the CPUs)
+    fitting = [t for t in sweep if 4 * int(t) <= effective]
+    best_fit = max(fitting, key=lambda t: sweep[t]["cfg2_gcups"]) if fitting else "1"
+    T = threads_per_server or int(best_fit)
 
     board = oracle.unpack(oracle.init_random(size, size, seed=3), size)
     t0 = time.perf_counter()
@@ -374,8 +393,11 @@ def cpu_baseline(size: int, turns: int, threads_per_server: int | None = None) -
     return {
         "value": round(cups / 1e9, 4),
         "unit": "GCUPS",
-        "cores": 4 * T,
+        "cores": 4 * T,  # = threads used: 4 servers x T goroutine-threads, <= effective_cpus
+        "threads": 4 * T,
         "threads_per_server": T,
+        "effective_cpus": effective,
+        "value_per_effective_cpu": round(cups / 1e9 / min(4 * T, effective), 4),
         "host_cores": nproc,
         **share,
         "cpu_model": model,
@@ -384,12 +406,14 @@ def cpu_baseline(size: int, turns: int, threads_per_server: int | None = None) -
         "kind": "port",
         "sample": (f"{size}x{size} random p=0.5 seed 3 (the bench board), {turns} turns of the "
                    f"reference algorithm at T = {T} goroutine-threads per server (the best T of the "
-                   f"sweep on configs[1]'s first 20 turns): byte cells, branchy torus wrap + /255, "
+                   f"sweep on configs[1]'s first 20 turns with 4T <= the job's {effective} CPUs): "
+                   f"byte cells, branchy torus wrap + /255, "
                    f"fresh rows per turn, 4 broker strips x {T} = {4 * T} worker threads (one pool "
                    f"per run), full-world copy per server per turn, per-turn alive scan; gob/TCP "
                    f"transport not timed; {dt:.1f} s"),
         "t_sweep": sweep,
         "best_threads_per_server": int(best_t),
+        "best_threads_per_server_within_cpus": int(best_fit),
         "cfg5_4096_first100": {"s": round(dt5, 4), "gcups": round(4096 * 4096 * 100 / dt5 / 1e9, 4),
                                "us_per_turn": round(dt5 / 100 * 1e6, 1),
                                "counts_match_golden": [int(x) for x in c5] == exp5,
@@ -402,7 +426,7 @@ def cpu_baseline(size: int, turns: int, threads_per_server: int | None = None) -
     }
 
 
-DIGEST_CHUNK_ROWS = 4096  # = oracle.DIGEST_CHUNK_ROWS (tests/test_bench_digest.py checks both)
+DIGEST_CHUNK_ROWS = 4096  # = oracle.DIGEST_CHUNK_ROWS (tests/test_tools.py checks both)
 
 
 def chunk_digests(words) -> list[bytes]:
@@ -589,7 +613,15 @@ def main():
     # host transport instead of RCCL, so N ranks can share the one GPU of a test box (RCCL refuses
     # two ranks on one device); the engine, its launch plan and the timed region are unchanged
     host_comm = os.environ.get("GOLHIP_HOST_COMM", "0") == "1" and world > 1
-    if host_comm:
+    # test hook (tests/test_gpu_rccl_ranks.py): GOLHIP_RCCL_SHARED_GPU=1 runs N REAL RCCL ranks on
+    # the one GPU of a test box: a distinct NCCL_HOSTID per rank makes RCCL treat the ranks as
+    # separate hosts and connect them through its network transport (loopback) instead of refusing
+    # "Duplicate GPU"; the engine, the process group, the timed region are the N > 1 code
+    rccl_shared = os.environ.get("GOLHIP_RCCL_SHARED_GPU", "0") == "1" and world > 1 and not host_comm
+    if rccl_shared:
+        os.environ["NCCL_HOSTID"] = f"golhip-bench-rank{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    if host_comm or rccl_shared:
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1 or a.pg_always:
@@ -606,10 +638,12 @@ def main():
             obj = [None]
             dist.broadcast_object_list(obj, src=0)  # the collective N > 1 runs before the engine
         # every rank on this node (torch.distributed.run's LOCAL_WORLD_SIZE): the timed region's
-        # barriers go through shared memory (--rccl-barrier keeps the process group's)
-        if (not a.rccl_barrier and int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) == world
-                and os.path.isdir("/dev/shm")):
-            SHM_BARRIER = ShmBarrier.create(rank, world, a.pg_timeout_s)
+        # barriers go through shared memory (--rccl-barrier, the same flag on every rank, keeps the
+        # process group's); every rank joins the set-up's vote whatever its local checks say
+        if not a.rccl_barrier:
+            local_ok = (int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) == world
+                        and os.path.isdir("/dev/shm"))
+            SHM_BARRIER = ShmBarrier.create(rank, world, a.pg_timeout_s, local_ok=local_ok)
     golhip.set_default_comm_timeout(a.comm_timeout_ms)
 
     width = a.size
@@ -667,6 +701,7 @@ def main():
     # without them and the launch durations come from a second, identical pass below
     eng.timing(False)
     dt = timed_steps(eng, a.steps, world)
+    timed_rank_s = list(RANK_TIMES)
     # regression canary: alive cells after exactly warmup + steps generations (deterministic for
     # the seed; compare across kernel versions)
     alive_timed = eng.alive_count()
@@ -689,7 +724,9 @@ def main():
         eng.sync()
         eng.timing(True)
         dti = timed_steps(eng, a.steps, world)
+        inst_rank_s = list(RANK_TIMES)
         kern_ms, launches, gens = eng.kernel_time()
+        edge_ms, edge_blocks = eng.edge_wait()
         eng.timing(False)
         alive_i = eng.alive_count()
         if alive_i != alive_timed:
@@ -703,6 +740,20 @@ def main():
                                 "events (roofline.avg_launch_us); value is the uninstrumented pass"}
     digest = board_digest(timed_words, world)
     del timed_words
+    # N > 1: what each rank's timed region was made of, so a scaling line explains its own
+    # efficiency -- the rank's wall time in the timed pass, and in the instrumented pass its
+    # HIP-event kernel span on the compute stream and the time that stream waited for the boundary
+    # bands (which wait for the halo exchange) after each block's interior
+    per_rank = None
+    if dist.is_initialized():
+        mine = {"rank": rank, "y0": int(eng.info.y0), "rows": int(local_rows),
+                "timed_ms": round(timed_rank_s[rank] * 1e3, 4)}
+        if not a.no_timing:
+            mine.update({"instrumented_ms": round(inst_rank_s[rank] * 1e3, 4),
+                         "kernel_span_ms": round(kern_ms, 4), "launches": launches,
+                         "edge_wait_ms": round(edge_ms, 4), "split_blocks": edge_blocks})
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
     total_updates = width * height * a.steps
     gcups = total_updates / dt / 1e9
     ms_per_step = dt * 1e3 / a.steps
@@ -924,7 +975,9 @@ def main():
             "untimed_generations_before_value": (
                 a.warmup + (a.warmup + a.steps + cold["preheat_turns"] if cold else 0)),
             "transport": "gloo host transport (test hook GOLHIP_HOST_COMM=1)" if host_comm else
-                         ("rccl" if world > 1 else
+                         ("rccl, every rank on one GPU (test hook GOLHIP_RCCL_SHARED_GPU=1: RCCL's "
+                          "network transport over loopback)" if rccl_shared else
+                          "rccl" if world > 1 else
                           "rccl ring of one (GOLHIP_RING_SELF=1)" if os.environ.get("GOLHIP_RING_SELF") == "1" else None),
             "process": {"gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                         "process_group": dist.get_backend() if dist.is_initialized() else None,
@@ -935,6 +988,7 @@ def main():
             "cold_start": cold,
             # the roofline's launch durations: an identical pass after the timed one, with events
             "instrumented_pass": instrumented,
+            "per_rank": per_rank,
             "roofline": roof,
             "hbm_roofline": hbm_roof,
             "cpu_baseline": cpu,
@@ -977,7 +1031,12 @@ if __name__ == "__main__":
         print(f"bench: rank {rank} failed: {e!r}; last engine call(s): {calls}", file=sys.stderr,
               flush=True)
         sys.stdout.flush()
-        # no interpreter teardown: after an RCCL failure the engine's communicator is left in
-        # place with work possibly queued behind a stuck transfer (golhip_engine.hip comm_abort);
-        # ending the process is what removes it
+        # after an RCCL failure: abort every engine's failed communicator (ncclCommAbort makes the
+        # RCCL kernels spinning on the stuck transfer exit: profiles/r05/r05d_stuck_rccl_receive_abort.log),
+        # then leave without the interpreter's teardown
+        for x in ENGINES:
+            try:
+                x.comm_abort()
+            except Exception:
+                pass
         os._exit(3)

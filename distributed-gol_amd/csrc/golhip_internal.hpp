@@ -5,25 +5,21 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <cstdlib>
+#include <cstddef>
 
 namespace golhip {
 
-// Two builds of the same sources (Makefile):
+// Two libraries from the same production sources (Makefile):
 //   lib/libgolhip.so         production: only the kernels the automatic planner runs (the
 //                            production drift stencil at every depth, gol_step1, the production
 //                            register-slab shapes); no tuning environment variable is read;
-//   lib_tuning/libgolhip.so  -DGOLHIP_TUNING: also the measured-and-rejected stencil variants,
-//                            the level-split and register-tile kernels, the other slab shapes and
-//                            the environment selectors of the A/B scripts (GOLHIP_VARIANT,
-//                            GOLHIP_SPLIT/TILE/SLAB, GOLHIP_BAND_ROWS, GOLHIP_FIXED_K,
-//                            GOLHIP_LDS_PAD, GOLHIP_STEP1).  Tests of those kernels and the
-//                            tuning scripts load it explicitly.
-#ifdef GOLHIP_TUNING
-constexpr bool kTuningBuild = true;
-#else
-constexpr bool kTuningBuild = false;
-#endif
+//   lib_tuning/libgolhip.so  the same objects PLUS the tuning-only translation units under
+//                            csrc/tuning/: the measured-and-rejected stencil variants, the
+//                            level-split and register-tile kernels, the other slab shapes, the
+//                            timestamping kernels, the fault-injection hooks and the environment
+//                            selectors of the A/B scripts.  Those TUs register themselves in
+//                            kernel_extras() (below) / engine_hooks() (golhip_engine.hpp) when the
+//                            library loads; the production sources never name the tuning build.
 
 // Device layout of one row strip (see DESIGN.md "Data layout in HBM"):
 //   torus width L = lcm(width, 128) bits, wd = L/32 uint32 words per row, LSB-first
@@ -56,8 +52,8 @@ struct StencilParams {
     // > 0 (gol_slab only; golhip_step_flips): EVERY generation g (0-based) of the launch writes its
     // flips to diff + g * diff_stride words (consecutive slots of the per-turn flips ring)
     int64_t diff_stride;
-    // tuning build only (null otherwise): gol_slab2's per-wave phase stamps, 8 uint64 per wave
-    // (golhip_tuning_stamps_ex, scripts/slab_stamps.py)
+    // null in production; the tuning library's stamp handles: gol_slab2's per-wave phase stamps,
+    // 8 uint64 per wave (golhip_tuning_stamps_ex, scripts/slab_stamps.py)
     uint64_t *stamp;
 };
 
@@ -124,34 +120,56 @@ inline int chunk_words(int K, int variant, bool counting = false) {
     return (d == 1 && K <= 16) ? 63 : 62 * d;
 }
 
-// Launch depths with a stencil instantiation, one translation unit each (stencil_k<K>.hip).
-#ifdef GOLHIP_TUNING
-// + K = 20 / 24 (the 62-word drift geometry; measured for the driver's 20-turn region)
-#define GOLHIP_STENCIL_DEPTHS(X) X(1) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(20) X(24) X(32)
-#else
+// Production launch depths, one translation unit each (stencil_k<K>.hip).  The tuning library adds
+// K = 20 / 24 through kernel_extras().
 #define GOLHIP_STENCIL_DEPTHS(X) X(1) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(32)
-#endif
 #define GOLHIP_X(K)                                                                           \
-    hipError_t launch_stencil_k##K(int variant, const uint32_t *in, uint32_t *out,            \
-                                   const StencilParams &p, unsigned long long *slots,        \
-                                   hipStream_t s);                                           \
-    const void *stencil_fn_k##K(int variant);                                                 \
-    hipError_t warm_stencil_k##K(int variant, hipStream_t s);
+    hipError_t launch_stencil_k##K(const uint32_t *in, uint32_t *out, const StencilParams &p, \
+                                   unsigned long long *slots, hipStream_t s);                \
+    const void *stencil_fn_k##K();                                                            \
+    hipError_t warm_stencil_k##K(hipStream_t s);
 GOLHIP_STENCIL_DEPTHS(GOLHIP_X)
 #undef GOLHIP_X
 
-// Tuning knob (GOLHIP_LDS_PAD = bytes of unused dynamic LDS per block, tuning build only): caps the
-// resident blocks per CU, to measure the stencil's sensitivity to occupancy.  0 in production.
-inline size_t lds_pad_bytes() {
-#ifdef GOLHIP_TUNING
-    const char *e = std::getenv("GOLHIP_LDS_PAD");
-    return e ? (size_t)std::atol(e) : (size_t)0;
-#else
-    return 0;
-#endif
-}
+// Kernels beyond the production set.  Empty in the production library; the tuning library's
+// TUs (csrc/tuning/) fill it from static initialisers when the library loads.  Every dispatcher
+// asks the production kernels first and falls back to an entry here (a null entry: the kernel is
+// not in this library).
+using StencilLaunchFn = hipError_t (*)(int variant, const uint32_t *in, uint32_t *out,
+                                       const StencilParams &p, unsigned long long *slots,
+                                       hipStream_t s);
+struct KernelExtras {
+    // per depth: every kernel variant of that depth (the tuning variants, and the depths
+    // production lacks: K = 20 / 24); fn / warm as stencil_fn_k / warm_stencil_k
+    StencilLaunchFn stencil[kMaxK + 1] = {};
+    const void *(*stencil_fn[kMaxK + 1])(int variant) = {};
+    hipError_t (*stencil_warm[kMaxK + 1])(int variant, hipStream_t s) = {};
+    // gol_step1 configurations other than the production one (GOLHIP_STEP1); null: production
+    hipError_t (*step1)(const uint32_t *in, uint32_t *out, const StencilParams &p,
+                        unsigned long long *slots, hipStream_t s) = nullptr;
+    const void *(*step1_fn)() = nullptr;
+    // the level-split kernel, the register tiles, the slab shapes and slab variants production
+    // lacks
+    bool (*split_supported)(int K, int S) = nullptr;
+    hipError_t (*split)(int K, int S, const uint32_t *in, uint32_t *out, const StencilParams &p,
+                        unsigned long long *slots, hipStream_t s) = nullptr;
+    hipError_t (*split_warm)(hipStream_t s) = nullptr;
+    bool (*tile_supported)(int K, int T) = nullptr;
+    hipError_t (*tile)(int K, int T, const uint32_t *in, uint32_t *out, const StencilParams &p,
+                       unsigned long long *slots, hipStream_t s) = nullptr;
+    bool (*slab_supported)(int K, int W, int S, int NC) = nullptr;
+    // also every slab launch with p.stamp set (the timestamping slab kernels)
+    hipError_t (*slab)(int K, int W, int S, int NC, const uint32_t *in, uint32_t *out,
+                       const StencilParams &p, unsigned long long *slots, hipStream_t s) = nullptr;
+    // bytes of unused dynamic LDS per stencil block (GOLHIP_LDS_PAD: caps resident blocks per CU)
+    size_t lds_pad = 0;
+};
+KernelExtras &kernel_extras();
 
-// Launch the K-generation stencil (K in GOLHIP_STENCIL_DEPTHS). count_slots (nullable) receives
+// Unused dynamic LDS per stencil block: 0 in production.
+inline size_t lds_pad_bytes() { return kernel_extras().lds_pad; }
+
+// Launch the K-generation stencil (a production depth, or one kernel_extras() adds). count_slots (nullable) receives
 // per-generation alive counts in kCountSlots slots per generation.
 hipError_t launch_stencil(int K, int variant, const uint32_t *in_row0, uint32_t *out_row0,
                           const StencilParams &p, unsigned long long *count_slots,

@@ -323,7 +323,12 @@ inline unsigned grid_for(int64_t n, int threads = 256, int64_t cap = 8192) {
 
 }  // namespace
 
-bool stencil_k_supported(int K) {
+KernelExtras &kernel_extras() {
+    static KernelExtras x;  // filled by the tuning library's TUs; empty in production
+    return x;
+}
+
+static bool prod_depth(int K) {
     switch (K) {
 #define GOLHIP_X(KK) case KK:
         GOLHIP_STENCIL_DEPTHS(GOLHIP_X)
@@ -333,38 +338,62 @@ bool stencil_k_supported(int K) {
     }
 }
 
-// The per-depth stencil launchers live in stencil_k<K>.hip (one TU per depth).
+bool stencil_k_supported(int K) {
+    return prod_depth(K) || (K >= 1 && K <= kMaxK && kernel_extras().stencil[K] != nullptr);
+}
+
+// The per-depth production launchers live in stencil_k<K>.hip (one TU per depth); any other
+// variant or depth is a kernel_extras() entry (the tuning library), or not in this library.
 hipError_t launch_stencil(int K, int variant, const uint32_t *in_row0, uint32_t *out_row0,
                           const StencilParams &p, unsigned long long *slots, hipStream_t s) {
-    switch (K) {
+    if (variant == kVariantProd) {
+        switch (K) {
 #define GOLHIP_X(KK) \
-    case KK: return launch_stencil_k##KK(variant, in_row0, out_row0, p, slots, s);
-        GOLHIP_STENCIL_DEPTHS(GOLHIP_X)
+    case KK: return launch_stencil_k##KK(in_row0, out_row0, p, slots, s);
+            GOLHIP_STENCIL_DEPTHS(GOLHIP_X)
 #undef GOLHIP_X
-        default: return hipErrorInvalidValue;
+            default: break;
+        }
     }
+    if (K >= 1 && K <= kMaxK && kernel_extras().stencil[K])
+        return kernel_extras().stencil[K](variant, in_row0, out_row0, p, slots, s);
+    return hipErrorInvalidValue;
 }
 
 hipError_t warm_stencils(int variant, hipStream_t s) {
     hipError_t e = hipSuccess;
+    const KernelExtras &x = kernel_extras();
+    for (int K = 1; K <= kMaxK && e == hipSuccess; ++K) {
+        if (variant != kVariantProd || !prod_depth(K)) {
+            if (x.stencil_warm[K]) e = x.stencil_warm[K](variant, s);
+            continue;
+        }
+        switch (K) {
 #define GOLHIP_X(KK) \
-    if (e == hipSuccess) e = warm_stencil_k##KK(variant, s);
-    GOLHIP_STENCIL_DEPTHS(GOLHIP_X)
+    case KK: e = warm_stencil_k##KK(s); break;
+            GOLHIP_STENCIL_DEPTHS(GOLHIP_X)
 #undef GOLHIP_X
-    if (e == hipSuccess) e = warm_stencil_split(s);
+            default: break;
+        }
+    }
+    if (e == hipSuccess && x.split_warm) e = x.split_warm(s);
     if (e == hipSuccess) e = warm_stencil_tile(s);
     return e;
 }
 
 int stencil_waves_per_cu(int K, int variant) {
     const void *fn = nullptr;
-    switch (K) {
+    if (variant == kVariantProd) {
+        switch (K) {
 #define GOLHIP_X(KK) \
-    case KK: fn = stencil_fn_k##KK(variant); break;
-        GOLHIP_STENCIL_DEPTHS(GOLHIP_X)
+    case KK: fn = stencil_fn_k##KK(); break;
+            GOLHIP_STENCIL_DEPTHS(GOLHIP_X)
 #undef GOLHIP_X
-        default: return 4;
+            default: break;
+        }
     }
+    if (!fn && K >= 1 && K <= kMaxK && kernel_extras().stencil_fn[K]) fn = kernel_extras().stencil_fn[K](variant);
+    if (!fn) return 4;
     int blocks = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, 256, lds_pad_bytes()) != hipSuccess || blocks < 1)
         return 4;

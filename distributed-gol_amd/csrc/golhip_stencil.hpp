@@ -1079,46 +1079,17 @@ hipError_t launch_step1_cfg(const uint32_t *in, uint32_t *out, const StencilPara
         hipLaunchKernelGGL((gol_step1<false, P, NT>), dim3(blocks), dim3(256), 0, s, in, out, p, slots);
     return hipGetLastError();
 }
-// Production gol_step1: 4 rows in flight, non-temporal stores (profiles/r01_tune_step1.txt).
-#ifndef GOLHIP_TUNING
+// Production gol_step1: 4 rows in flight, non-temporal stores (profiles/r01_tune_step1.txt).  The
+// tuning library can register other prefetch depths / cache policies (GOLHIP_STEP1).
 inline hipError_t launch_step1(const uint32_t *in, uint32_t *out, const StencilParams &p,
                                unsigned long long *slots, hipStream_t s) {
+    if (const auto f = kernel_extras().step1) return f(in, out, p, slots, s);
     return launch_step1_cfg<4, 2>(in, out, p, slots, s);
 }
-inline const void *step1_fn() { return (const void *)gol_step1<false, 4, 2>; }
-#else
-// Tuning build: GOLHIP_STEP1 = P*10 + NT selects the prefetch depth and cache policy (read once;
-// unset = the production configuration).
-inline int step1_config() {
-    static const int cfg = [] {
-        const char *e = std::getenv("GOLHIP_STEP1");
-        return e ? std::atoi(e) : 42;
-    }();
-    return cfg;
-}
-#define GOLHIP_STEP1_CONFIGS(X) \
-    X(20, 2, 0) X(22, 2, 2) X(30, 3, 0) X(32, 3, 2) X(40, 4, 0) X(41, 4, 1) X(42, 4, 2) \
-    X(43, 4, 3) X(60, 6, 0) X(62, 6, 2) X(80, 8, 0) X(82, 8, 2)
-inline hipError_t launch_step1(const uint32_t *in, uint32_t *out, const StencilParams &p,
-                               unsigned long long *slots, hipStream_t s) {
-    switch (step1_config()) {
-#define GOLHIP_X(C, P, NT) \
-    case C: return launch_step1_cfg<P, NT>(in, out, p, slots, s);
-        GOLHIP_STEP1_CONFIGS(GOLHIP_X)
-#undef GOLHIP_X
-        default: return launch_step1_cfg<4, 2>(in, out, p, slots, s);
-    }
-}
 inline const void *step1_fn() {
-    switch (step1_config()) {
-#define GOLHIP_X(C, P, NT) \
-    case C: return (const void *)gol_step1<false, P, NT>;
-        GOLHIP_STEP1_CONFIGS(GOLHIP_X)
-#undef GOLHIP_X
-        default: return (const void *)gol_step1<false, 4, 2>;
-    }
+    if (const auto f = kernel_extras().step1_fn) return f();
+    return (const void *)gol_step1<false, 4, 2>;
 }
-#endif
 
 template <int K, bool SKEW, int D, int PF = 0, bool DR = false, int ZIP = 1, bool HH = kHalfHalo<K, D>,
           bool FILLU = true, bool ALLOW_LD = false, bool PRE = false, bool MASK = false, bool STAMP = false>
@@ -1178,110 +1149,6 @@ const void *prod_fn() {
     else return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1>;
 }
 
-#ifndef GOLHIP_TUNING
-// Production build: the production kernel whatever the handle's variant (always kVariantProd there).
-template <int K>
-hipError_t launch_variant(int, const uint32_t *in, uint32_t *out, const StencilParams &p,
-                          unsigned long long *slots, hipStream_t s) {
-    return launch_prod<K>(in, out, p, slots, s);
-}
-template <int K>
-const void *variant_fn(int) {
-    return prod_fn<K>();
-}
-#else
-// Tuning build: every measured variant (GOLHIP_VARIANT, tests/test_gpu_tuning.py, scripts/ab_*.py).
-template <int K>
-hipError_t launch_variant(int variant, const uint32_t *in, uint32_t *out, const StencilParams &p,
-                          unsigned long long *slots, hipStream_t s) {
-    switch (variant) {
-        case kVariantChain: return launch_stencil_k<K, false, 1>(in, out, p, slots, s);
-        case kVariantSkewD2: return launch_stencil_k<K, true, 2>(in, out, p, slots, s);
-        case kVariantChainD2: return launch_stencil_k<K, false, 2>(in, out, p, slots, s);
-        case kVariantSkewLdsPf: return launch_stencil_k<K, true, 1, 1>(in, out, p, slots, s);
-        case kVariantChainLdsPf:
-            if constexpr (K == 1) return launch_step1(in, out, p, slots, s);  // production K = 1
-            return launch_stencil_k<K, false, 1, 1>(in, out, p, slots, s);
-        case kVariantSkewLdsD2: return launch_stencil_k<K, true, 2, 1>(in, out, p, slots, s);
-        case kVariantChainLdsD2: return launch_stencil_k<K, false, 2, 1>(in, out, p, slots, s);
-        case kVariantDriftLds:
-            if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
-            else if constexpr (K > 16) return launch_stencil_k<K, false, 1, 1, false, 1, kHalfHalo<K, 1>, true, true>(in, out, p, slots, s);
-            else return launch_stencil_k<K, false, 1, 1, true, 1, true, true, true>(in, out, p, slots, s);
-        case kVariantDrift62:
-            if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
-            else return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true>(in, out, p, slots, s);
-        case kVariantProd:  // per depth and counting: the fastest measured (golhip_internal.hpp)
-            return launch_prod<K>(in, out, p, slots, s);
-        case kVariantStamp:  // the production kernel with per-wave timestamps (p.diff: stamps)
-            if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
-            else if constexpr (K <= 16) {
-                if (prod_pre(K, slots != nullptr))
-                    return launch_stencil_k<K, false, 1, 1, true, 1, false, true, false, true, false, true>(in, out, p, slots, s);
-                return launch_stencil_k<K, false, 1, 1, true, 1, false, true, false, false, false, true>(in, out, p, slots, s);
-            } else return launch_stencil_k<K, false, 1, 1, true, 1, false, true, false, false, false, true>(in, out, p, slots, s);
-        case kVariantDriftNoFill:
-            if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
-            else return launch_stencil_k<K, false, 1, 1, (K <= 16), 1, kHalfHalo<K, 1>, false>(in, out, p, slots, s);
-        case kVariantProdMask:  // production with the idle lanes of the last chunk masked off
-            if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
-            else if constexpr (K <= 16) {
-                if (prod_pre(K, slots != nullptr))
-                    return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true, true, true>(in, out, p, slots, s);
-                return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true, false, true>(in, out, p, slots, s);
-            } else return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true, false, true>(in, out, p, slots, s);
-        case kVariantPre63:  // pre-shifted rows, 63-word chunks (K <= 16; drift62 above)
-            if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
-            else if constexpr (K > 16) return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true>(in, out, p, slots, s);
-            else return launch_stencil_k<K, false, 1, 1, true, 1, false, true, true, true>(in, out, p, slots, s);
-        case kVariantDriftZip:
-            if constexpr (K == 1) return launch_step1(in, out, p, slots, s);
-            else return launch_stencil_k<K, false, 1, 1, true, 2, false>(in, out, p, slots, s);
-        default: return launch_stencil_k<K, true, 1>(in, out, p, slots, s);
-    }
-}
-
-template <int K>
-const void *variant_fn(int variant) {
-    switch (variant) {
-        case kVariantChain: return (const void *)gol_stencil<K, false, false, 1, 0, kHalfHalo<K, 1>>;
-        case kVariantSkewD2: return (const void *)gol_stencil<K, false, true, 2, 0, kHalfHalo<K, 2>>;
-        case kVariantChainD2: return (const void *)gol_stencil<K, false, false, 2, 0, kHalfHalo<K, 2>>;
-        case kVariantSkewLdsPf: return (const void *)gol_stencil<K, false, true, 1, 1, kHalfHalo<K, 1>>;
-        case kVariantChainLdsPf:
-            if constexpr (K == 1) return step1_fn();
-            return (const void *)gol_stencil<K, false, false, 1, 1, kHalfHalo<K, 1>>;
-        case kVariantSkewLdsD2: return (const void *)gol_stencil<K, false, true, 2, 1, kHalfHalo<K, 2>>;
-        case kVariantChainLdsD2: return (const void *)gol_stencil<K, false, false, 2, 1, kHalfHalo<K, 2>>;
-        case kVariantDriftLds:
-            if constexpr (K == 1) return step1_fn();
-            else return (const void *)gol_stencil<K, false, false, 1, 1, kHalfHalo<K, 1>, (K <= 16)>;
-        case kVariantDrift62:
-            if constexpr (K == 1) return step1_fn();
-            else return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1>;
-        case kVariantProd: return prod_fn<K>();
-        case kVariantStamp:
-            if constexpr (K == 1) return step1_fn();
-            else if constexpr (prod_pre(K)) return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1, true, false, 0, true, false, true>;
-            else return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1, true, false, 0, false, false, true>;
-        case kVariantDriftNoFill:
-            if constexpr (K == 1) return step1_fn();
-            else return (const void *)gol_stencil<K, false, false, 1, 1, kHalfHalo<K, 1>, (K <= 16), 1, false>;
-        case kVariantProdMask:
-            if constexpr (K == 1) return step1_fn();
-            else if constexpr (prod_pre(K)) return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1, true, false, 0, true, true>;
-            else return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1, true, false, 0, false, true>;
-        case kVariantPre63:
-            if constexpr (K == 1) return step1_fn();
-            else if constexpr (K > 16) return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1>;
-            else return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 1, true, false, 0, true>;
-        case kVariantDriftZip:
-            if constexpr (K == 1) return step1_fn();
-            else return (const void *)gol_stencil<K, false, false, 1, 1, false, true, 2>;
-        default: return (const void *)gol_stencil<K, false, true, 1, 0, kHalfHalo<K, 1>>;
-    }
-}
-#endif  // GOLHIP_TUNING
 
 template <int K, int S>
 hipError_t launch_split_ks(const uint32_t *in, uint32_t *out, const StencilParams &p,
@@ -1305,19 +1172,19 @@ hipError_t launch_split_ks(const uint32_t *in, uint32_t *out, const StencilParam
 
 }  // namespace
 
-// Defines launch_stencil_k<K> / stencil_fn_k<K> (declared in golhip_internal.hpp) in the TU
-// that includes this header for one depth.
+// Defines the production launcher of depth K (launch_stencil_k<K> / stencil_fn_k<K> /
+// warm_stencil_k<K>, declared in golhip_internal.hpp) in the TU that includes this header for one
+// depth.
 #define GOLHIP_DEFINE_STENCIL_K(K)                                                            \
-    hipError_t launch_stencil_k##K(int variant, const uint32_t *in, uint32_t *out,              \
-                                   const StencilParams &p, unsigned long long *slots,          \
-                                   hipStream_t s) {                                            \
-        return launch_variant<K>(variant, in, out, p, slots, s);                              \
+    hipError_t launch_stencil_k##K(const uint32_t *in, uint32_t *out, const StencilParams &p, \
+                                   unsigned long long *slots, hipStream_t s) {                \
+        return launch_prod<K>(in, out, p, slots, s);                                          \
     }                                                                                          \
-    const void *stencil_fn_k##K(int variant) { return variant_fn<K>(variant); }                \
-    hipError_t warm_stencil_k##K(int variant, hipStream_t s) {                                  \
+    const void *stencil_fn_k##K() { return prod_fn<K>(); }                                     \
+    hipError_t warm_stencil_k##K(hipStream_t s) {                                              \
         StencilParams p{};                                                                      \
         p.nchunks = 1; /* nbands = 0: every wave returns at once */                            \
-        return launch_variant<K>(variant, nullptr, nullptr, p, nullptr, s);                     \
+        return launch_prod<K>(nullptr, nullptr, p, nullptr, s);                                 \
     }
 
 }  // namespace golhip

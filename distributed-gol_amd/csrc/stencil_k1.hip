@@ -1,4 +1,4 @@
-// stencil_k1.hip -- the 1-generation stencil launchers (every variant), one TU per launch depth.
+// stencil_k1.hip -- the production 1-generation stencil launcher, one TU per launch depth.
 #include "golhip_stencil.hpp"
 
 namespace golhip {

@@ -1,4 +1,4 @@
-// stencil_k10.hip -- the 10-generation stencil launchers (every variant), one TU per launch depth.
+// stencil_k10.hip -- the production 10-generation stencil launcher, one TU per launch depth.
 #include "golhip_stencil.hpp"
 
 namespace golhip {

@@ -1,4 +1,4 @@
-// stencil_k12.hip -- the 12-generation stencil launchers (every variant), one TU per launch depth.
+// stencil_k12.hip -- the production 12-generation stencil launcher, one TU per launch depth.
 #include "golhip_stencil.hpp"
 
 namespace golhip {

@@ -1,4 +1,4 @@
-// stencil_k14.hip -- the 14-generation stencil launchers (every variant), one TU per launch depth.
+// stencil_k14.hip -- the production 14-generation stencil launcher, one TU per launch depth.
 #include "golhip_stencil.hpp"
 
 namespace golhip {

@@ -1,4 +1,4 @@
-// stencil_k16.hip -- the 16-generation stencil launchers (every variant), one TU per launch depth.
+// stencil_k16.hip -- the production 16-generation stencil launcher, one TU per launch depth.
 #include "golhip_stencil.hpp"
 
 namespace golhip {

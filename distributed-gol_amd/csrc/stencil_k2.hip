@@ -1,4 +1,4 @@
-// stencil_k2.hip -- the 2-generation stencil launchers (every variant), one TU per launch depth.
+// stencil_k2.hip -- the production 2-generation stencil launcher, one TU per launch depth.
 #include "golhip_stencil.hpp"
 
 namespace golhip {

@@ -1,4 +1,4 @@
-// stencil_k32.hip -- the 32-generation stencil launchers (every variant), one TU per launch depth.
+// stencil_k32.hip -- the production 32-generation stencil launcher, one TU per launch depth.
 #include "golhip_stencil.hpp"
 
 namespace golhip {

@@ -1,4 +1,4 @@
-// stencil_k4.hip -- the 4-generation stencil launchers (every variant), one TU per launch depth.
+// stencil_k4.hip -- the production 4-generation stencil launcher, one TU per launch depth.
 #include "golhip_stencil.hpp"
 
 namespace golhip {

@@ -1,4 +1,4 @@
-// stencil_k6.hip -- the 6-generation stencil launchers (every variant), one TU per launch depth.
+// stencil_k6.hip -- the production 6-generation stencil launcher, one TU per launch depth.
 #include "golhip_stencil.hpp"
 
 namespace golhip {

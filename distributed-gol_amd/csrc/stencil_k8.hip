@@ -1,4 +1,4 @@
-// stencil_k8.hip -- the 8-generation stencil launchers (every variant), one TU per launch depth.
+// stencil_k8.hip -- the production 8-generation stencil launcher, one TU per launch depth.
 #include "golhip_stencil.hpp"
 
 namespace golhip {

@@ -39,6 +39,7 @@ EXPORTS = [
     "golhip_version", "golhip_strerror", "golhip_device_count", "golhip_strip_bounds",
     "golhip_halo_plan",
     "golhip_create", "golhip_create_strips", "golhip_nccl_unique_id", "golhip_create_rank",
+    "golhip_comm_abort", "golhip_edge_wait",
     "golhip_create_rank_host", "golhip_destroy",
     "golhip_last_error", "golhip_get_info", "golhip_load_bytes", "golhip_init_random",
     "golhip_store_bytes", "golhip_store_words", "golhip_load_words", "golhip_step",
@@ -201,8 +202,10 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
         "golhip_set_graphs": ([H, i32], i32),
         "golhip_set_count_window": ([H, i32], i32),
         "golhip_set_comm_timeout": ([H, i64], i32),
+        "golhip_comm_abort": ([H], i32),
         "golhip_timing": ([H, i32], i32),
         "golhip_kernel_time": ([H, ctypes.POINTER(ctypes.c_double), i64p, i64p], i32),
+        "golhip_edge_wait": ([H, ctypes.POINTER(ctypes.c_double), i64p], i32),
         "golhip_launch_plan": ([i64, i64, i32, i32, i64, ctypes.c_void_p, ctypes.c_size_t,
                                 ctypes.POINTER(ctypes.c_size_t)], i32),
         "golhip_launch_kind": ([H, i32, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], i32),
@@ -216,6 +219,8 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
     _libs[key] = L
     if path is None:
         _lib = L
+    if _default_comm_timeout_ms is not None:  # set_default_comm_timeout reaches every library
+        L.golhip_set_comm_timeout(None, _default_comm_timeout_ms)
     return L
 
 
@@ -225,11 +230,25 @@ def tuning_library() -> ctypes.CDLL:
     return load_library(TUNING_LIB_PATH)
 
 
+_default_comm_timeout_ms: int | None = None
+
+
 def set_default_comm_timeout(ms: int, lib: ctypes.CDLL | None = None) -> None:
-    """golhip_set_comm_timeout(NULL, ms): the RCCL deadline of engines created from now on."""
-    rc = (lib or load_library()).golhip_set_comm_timeout(None, int(ms))
-    if rc != OK:
-        raise GolHipError(rc, "set_comm_timeout: invalid argument")
+    """golhip_set_comm_timeout(NULL, ms): the RCCL deadline of engines created from now on, in every
+    library loaded now or later (an Engine(..., lib=tuning_library()) in rank mode included), or
+    only in `lib` when given."""
+    global _default_comm_timeout_ms
+    if int(ms) <= 0:
+        raise GolHipError(ERR_ARG, "set_comm_timeout: invalid argument")
+    if lib is not None:
+        libs = [lib]
+    else:
+        _default_comm_timeout_ms = int(ms)
+        libs = list(_libs.values()) or [load_library()]
+    for L in libs:
+        rc = L.golhip_set_comm_timeout(None, int(ms))
+        if rc != OK:
+            raise GolHipError(rc, "set_comm_timeout: invalid argument")
 
 
 class _CallLog:
@@ -575,6 +594,11 @@ class Engine:
         """Deadline of waits on RCCL-dependent work (rank mode): ERR_RCCL when it passes."""
         self._check(self._L.golhip_set_comm_timeout(self._h, int(ms)))
 
+    def comm_abort(self):
+        """After GOLHIP_ERR_RCCL: ncclCommAbort the handle's communicator (RCCL aborts its operations
+        still running on the device), so the streams can drain before close()."""
+        self._check(self._L.golhip_comm_abort(self._h))
+
     def launch_kind(self, k: int, counts: bool = False) -> tuple[str, int]:
         """The kernel a k-deep launch runs (with / without per-generation counts): ("stream", 0),
         ("split", S), ("tile", T) or ("slab", [10000 NC +] 100 W + S)."""
@@ -588,6 +612,13 @@ class Engine:
 
     def timing(self, enable: bool):
         self._check(self._L.golhip_timing(self._h, int(enable)))
+
+    def edge_wait(self) -> tuple[float, int]:
+        """With timing on (split boards): ms the compute stream waited for the boundary bands after
+        each block's interior, summed, and the number of blocks (golhip_edge_wait)."""
+        ms, blocks = ctypes.c_double(), ctypes.c_int64()
+        self._check(self._L.golhip_edge_wait(self._h, ctypes.byref(ms), ctypes.byref(blocks)))
+        return ms.value, blocks.value
 
     def kernel_time(self) -> tuple[float, int, int]:
         ms, launches, gens = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()

@@ -95,15 +95,13 @@ int golhip_create(int width, int height, int ngpus, int k, golhip_t *out);
 int golhip_create_strips(int width, int height, int nstrips, int ndevices, int k, golhip_t *out);
 /* One process per GPU: rank `rank` of `world_size`, on HIP device `device`. nccl_id: the
  * GOLHIP_NCCL_ID_BYTES produced by golhip_nccl_unique_id() on rank 0 (NULL if world_size == 1).
- * Test hook: with world_size == 1 and the environment variable GOLHIP_RING_SELF=1 the board is a
- * ring of ONE halo'd strip whose halos go through RCCL send/recv to itself (the rank-mode path
- * on a single GPU); GOLHIP_RING_SELF=2 is the same ring with every golhip_step ending in a 20 s
- * stall of the compute stream (a rank whose work does not finish: the fail-fast test of
- * golhip_set_comm_timeout).
+ * Test hook: with world_size == 1 and the environment variable GOLHIP_RING_SELF set (nonzero) the
+ * board is a ring of ONE halo'd strip whose halos go through RCCL send/recv to itself (the
+ * rank-mode path on a single GPU).
  * The communicator is non-blocking: a rank whose peers never join fails after the comm timeout.
  * GOLHIP_RING_SELF and GOLHIP_STAGE_BYTES (the transfer stage's size in bytes, read at create;
  * tests shrink it to force many row chunks) are the only environment variables the production
- * library reads. */
+ * library reads (fault injection for the fail-fast tests is in the tuning library only). */
 int golhip_nccl_unique_id(uint8_t *out /* GOLHIP_NCCL_ID_BYTES */);
 int golhip_create_rank(int width, int height, int rank, int world_size, int device, int k,
                        const uint8_t *nccl_id, golhip_t *out);
@@ -244,17 +242,28 @@ int golhip_set_count_window(golhip_t h, int generations);
  * modelled time of the stencil work queued since the last sync.  When it passes (or RCCL reports an
  * asynchronous error) the call returns GOLHIP_ERR_RCCL, with golhip_last_error naming the rank,
  * the pending operation, its peers, K and its byte count; the handle then only accepts
- * golhip_destroy.  A communicator whose set-up failed is aborted (nothing of it is on the device);
- * after set-up it is left in place -- RCCL kernels may still be queued behind the stalled work and
- * an abort would free state they use -- and the caller should end the process (bench.py: _exit).  h == NULL sets the default of later creates (120000).
+ * golhip_comm_abort / golhip_destroy.  A communicator whose set-up failed is aborted (nothing of
+ * it is on the device); after set-up it is left in place until golhip_comm_abort or golhip_destroy
+ * (which aborts a failed communicator, then drains the streams within the timeout) or the end of
+ * the process.  h == NULL sets the default of later creates (120000).
  * The reference has no such bound: a dead server stalls Broker.Publish (broker/broker.go:58-84). */
 int golhip_set_comm_timeout(golhip_t h, int64_t ms);
+/* After GOLHIP_ERR_RCCL on a rank-mode handle: ncclCommAbort its communicator (RCCL aborts the
+ * operations of it still running on the device, so a receive whose send never comes stops
+ * spinning), after which golhip_destroy can drain the handle's streams and free its memory.
+ * GOLHIP_ERR_STATE if the communicator has not failed. */
+int golhip_comm_abort(golhip_t h);
 int golhip_sync(golhip_t h);                         /* wait for all queued device work */
 /* HIP-event timing of golhip_step calls on the handle's first strip (one event pair per call
  * around its back-to-back stencil launches); kernel_time reports the summed span, the number of
  * stencil launch blocks and generations. */
 int golhip_timing(golhip_t h, int enable);
 int golhip_kernel_time(golhip_t h, double *total_ms, int64_t *launches, int64_t *generations);
+/* With timing on, on a board held as halo'd row strips (rank mode): the summed time the first
+ * strip's compute stream waited, after each block's interior launch, for that block's two boundary
+ * bands -- which wait for the halo exchange -- and the number of such blocks.  The part of a
+ * rank's time its neighbours and the transport cost it (the N > 1 bench line's per-rank data). */
+int golhip_edge_wait(golhip_t h, double *total_ms, int64_t *blocks);
 
 #ifdef __cplusplus
 }

@@ -140,6 +140,9 @@ class FakeEngine:
     def kernel_time(self):
         return self.t_ms, self.launches, self.gens
 
+    def edge_wait(self):
+        return 0.0, self.launches
+
     def alive_count(self):
         import torch
         import torch.distributed as dist
@@ -222,6 +225,15 @@ def test_bench_rank_path_cpu(tmp_path, world):
     assert line["process"]["barrier"] == "shared memory", line["process"]
     assert set(Path("/dev/shm").glob("golhip_bench_*")) <= shm_before
     assert line["untimed_generations_before_value"] == 5 + 25 + line["cold_start"]["preheat_turns"]
+    # per-rank data: every rank's timed-region and instrumented wall time, kernel span, edge wait
+    pr = line["per_rank"]
+    assert [r["rank"] for r in pr] == list(range(world)), pr
+    assert sum(r["rows"] for r in pr) == 4096 * world and [r["y0"] for r in pr] == sorted(r["y0"] for r in pr)
+    for r in pr:
+        assert r["timed_ms"] > 0 and r["instrumented_ms"] > 0 and r["kernel_span_ms"] > 0, r
+        assert r["launches"] >= 1 and r["edge_wait_ms"] >= 0 and r["split_blocks"] >= 1, r
+    # the line's value is the max over the ranks' timed regions
+    assert abs(line["ms_per_step"] * 20 - max(r["timed_ms"] for r in pr)) < 1e-3 * 20 + 1e-6, (line["ms_per_step"], pr)
 
 
 def test_bench_rank_path_cpu_process_group_barrier(tmp_path):

@@ -40,11 +40,27 @@ def test_library_is_gfx950_code(golhip):
     assert b"gfx950" in data
 
 
-# the tuning build's selectors (golhip_internal.hpp): the production library must not even hold
-# their names, so a stray environment variable cannot change its kernels
+# the tuning library's selectors and fault hooks (csrc/tuning/engine_tuning.hip): the production
+# library must not even hold their names, so a stray environment variable cannot change its kernels
 TUNING_SELECTORS = ["GOLHIP_VARIANT", "GOLHIP_SPLIT", "GOLHIP_TILE", "GOLHIP_SLAB", "GOLHIP_BAND_ROWS",
                     "GOLHIP_FIXED_K", "GOLHIP_LDS_PAD", "GOLHIP_STEP1", "GOLHIP_GRAPHS",
-                    "GOLHIP_COUNT_WINDOW"]
+                    "GOLHIP_COUNT_WINDOW", "GOLHIP_FAULT"]
+
+
+def test_production_sources_never_name_the_tuning_build():
+    """Tuning-only code lives in tuning-only translation units (csrc/tuning/), which the production
+    library does not link: no production source holds a GOLHIP_TUNING switch, and the production
+    library exports no tuning symbol."""
+    csrc = PKG / "csrc"
+    prod_sources = [p for p in csrc.iterdir() if p.suffix in (".hip", ".hpp")]
+    assert len(prod_sources) >= 10
+    for p in prod_sources:
+        text = p.read_text()
+        assert "GOLHIP_TUNING" not in text and "kTuningBuild" not in text, p.name
+    make = (PKG / "Makefile").read_text()
+    assert "-DGOLHIP_TUNING" not in make
+    out = subprocess.check_output(["nm", "-D", "--defined-only", str(PKG / "lib" / "libgolhip.so")], text=True)
+    assert "golhip_tuning" not in out
 
 
 def test_production_library_reads_only_documented_hooks():

@@ -3,10 +3,21 @@ GOLHIP_ERR_RCCL within its deadline (golhip_set_comm_timeout), naming the pendin
 instead of hanging the run (the reference has no such bound: a dead server stalls
 Broker.Publish forever, broker/broker.go:58-84).
 
-Each case runs in a FRESH process under its own time limit, so a failure of the deadline itself
-ends in a killed child, not a hung test session:
-  * stalled rank: the ring-of-one hook GOLHIP_RING_SELF=2 ends every step in a 20 s stall of the
-    compute stream, so the sync waits past its deadline;
+Each case runs in FRESH processes under their own time limits, so a failure of the deadline itself
+ends in a killed child, not a hung test session.  Fault injection is in the tuning library only
+(csrc/tuning/engine_tuning.hip, GOLHIP_FAULT); the engine code under test is the production code
+both libraries share.
+  * stuck receive: TWO real RCCL ranks on this one GPU (a distinct NCCL_HOSTID per rank makes RCCL
+    build a 2-rank communicator over its network transport instead of refusing "Duplicate GPU");
+    rank 1 leaves the first send of every halo exchange out of its RCCL group (GOLHIP_FAULT=
+    skip_send), so rank 0's receive never completes -- the path a real multi-GPU hang takes: an
+    RCCL kernel spinning on an unmatched receive.  Both ranks must fail at the deadline with the
+    first incomplete exchange named, golhip_comm_abort (rank 0) / golhip_destroy (rank 1) must
+    release the spinning RCCL kernels (ncclCommAbort), the streams must drain and both processes
+    exit 0 (round 4 claimed an abort with RCCL work queued faults the GPU; measured here, it does
+    not: profiles/r05/r05d_stuck_rccl_receive_abort.log);
+  * stalled rank: the ring of one (GOLHIP_RING_SELF=1) whose every step ends in a 20 s stall of the
+    compute stream (GOLHIP_FAULT=stall), so the sync waits past its deadline;
   * init: rank 0 of a 2-rank communicator whose rank 1 never joins -- ncclCommInitRankConfig
     (non-blocking) never finishes its set-up, and is aborted (nothing of it runs on the device).
 """
@@ -34,7 +45,7 @@ try:
     if case == "stall":
         # created under the default deadline (a first RCCL set-up in a fresh process can take
         # seconds), then the handle's own deadline
-        e = golhip.Engine(640, 64, k=4, rank=0, world_size=1, device=0)
+        e = golhip.Engine(640, 64, k=4, rank=0, world_size=1, device=0, lib=golhip.tuning_library())
         e.set_comm_timeout(timeout_ms)
         out["halo_rows"] = e.info.halo_rows
         e.init_random(5)
@@ -67,12 +78,72 @@ print(json.dumps(out), flush=True)
 os._exit(0)  # as bench.py after an RCCL failure: no interpreter teardown behind a stalled stream
 """
 
+# One rank of a real 2-rank RCCL communicator on this GPU (argv: pkg rank timeout_ms idfile).
+CHILD_RANK = r"""
+import faulthandler, json, os, sys, time
+pkg, rank, timeout_ms, idfile = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
+sys.path.insert(0, pkg)
+T0 = time.perf_counter()
+def log(msg):  # progress on stderr: where a killed child was
+    print(f"[rank {rank} +{time.perf_counter() - T0:.2f}s] {msg}", file=sys.stderr, flush=True)
+faulthandler.dump_traceback_later(75, exit=False)  # the Python stack of a child about to be killed
+import torch  # one HIP runtime per process (golhip.py)
+import golhip
+out = {"rank": rank}
+L = golhip.tuning_library()
+if rank == 0:
+    nid = golhip.nccl_unique_id()  # rank 0 hosts the bootstrap root
+    with open(idfile + ".tmp", "wb") as f:
+        f.write(nid)
+    os.rename(idfile + ".tmp", idfile)
+else:
+    t = time.time()
+    while not os.path.exists(idfile) and time.time() - t < 60:
+        time.sleep(0.05)
+    nid = open(idfile, "rb").read()
+t0 = time.perf_counter()
+# created under the default deadline (the set-up of a fresh communicator can take seconds), then
+# the handle's own deadline
+log("creating")
+e = golhip.Engine(640, 128, k=4, rank=rank, world_size=2, device=0, nccl_id=nid, lib=L)
+out["create_seconds"] = time.perf_counter() - t0
+e.set_comm_timeout(timeout_ms)
+e.init_random(5)
+log("stepping")
+t0 = time.perf_counter()
+try:
+    out["counts"] = [int(c) for c in e.step(9, counts=True)]
+    e.sync()
+    out["completed"] = True
+except golhip.GolHipError as err:
+    out["code"] = err.code
+    out["msg"] = str(err)
+    out["last_call"] = e.last_call
+out["seconds"] = time.perf_counter() - t0
+log(f"step returned: {out.get('code', 'ok')}: {out.get('msg', '')}")
+print(json.dumps(out), flush=True)  # the result so far, in case the teardown below is killed
+if "code" in out and os.environ.get("GOLHIP_TEST_ABORT", "1") == "1":
+    t1 = time.perf_counter()
+    if rank == 0:  # explicitly; rank 1 leaves it to golhip_destroy, which aborts a failed communicator
+        log("golhip_comm_abort")
+        e.comm_abort()  # ncclCommAbort: RCCL aborts its operations still running on the device
+    log("golhip_destroy")
+    e.close()  # aborts a failed communicator, drains the streams (bounded by the deadline), frees
+    log("closed")
+    out["abort_close_seconds"] = time.perf_counter() - t1
+    out["drained"] = True
+    print(json.dumps(out), flush=True)
+os._exit(0)
+"""
 
-def run_child(case, timeout_ms, ring_self=None):
+
+def run_child(case, timeout_ms, fault=None):
     env = dict(os.environ)
     env.pop("GOLHIP_RING_SELF", None)
-    if ring_self:
-        env["GOLHIP_RING_SELF"] = ring_self
+    env.pop("GOLHIP_FAULT", None)
+    if fault:
+        env["GOLHIP_RING_SELF"] = "1"
+        env["GOLHIP_FAULT"] = fault
     p = subprocess.run(["timeout", "-k", "10", "150", sys.executable, "-c", CHILD, str(PKG), case,
                         str(timeout_ms)], env=env, capture_output=True, text=True, timeout=200)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
@@ -80,15 +151,66 @@ def run_child(case, timeout_ms, ring_self=None):
     return json.loads(lines[-1])
 
 
+def rccl_shared_gpu_env(rank: int) -> dict:
+    """Environment of one rank of a multi-rank RCCL communicator on this single GPU: a distinct
+    NCCL_HOSTID per rank (RCCL then treats the ranks as separate hosts and connects them through
+    its network transport, over loopback)."""
+    env = dict(os.environ)
+    for k in ("GOLHIP_RING_SELF", "GOLHIP_FAULT"):
+        env.pop(k, None)
+    env["NCCL_HOSTID"] = f"golhip-test-rank{rank}"
+    env.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    return env
+
+
+@pytest.mark.timeout(240)
+def test_stuck_rccl_receive_fails_at_the_deadline_and_aborts(golhip, tmp_path):
+    timeout_ms = 3000
+    idfile = str(tmp_path / "nccl.id")
+    procs = []
+    for rank in (0, 1):
+        env = rccl_shared_gpu_env(rank)
+        if rank == 1:
+            env["GOLHIP_FAULT"] = "skip_send"
+        procs.append(subprocess.Popen(["timeout", "-k", "10", "90", sys.executable, "-c", CHILD_RANK, str(PKG),
+                                       str(rank), str(timeout_ms), idfile], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    res, outs = [], []
+    for p in procs:
+        so, se = p.communicate(timeout=200)
+        outs.append((p.returncode, so, se))
+    for rc, so, se in outs:  # both ranks' logs in any failure message
+        print(f"rc={rc}\n{so[-3000:]}\n{se[-6000:]}")
+    for rc, so, se in outs:
+        lines = [ln for ln in so.splitlines() if ln.startswith("{")]
+        assert rc == 0 and lines, (rc, so[-2000:], se[-3000:])
+        res.append(json.loads(lines[-1]))
+    print(json.dumps(res))
+    for r in res:
+        # every rank fails at its deadline (with the modelled allowance for its queued work) --
+        # not after the 150 s child limit, and without completing the call
+        assert not r.get("completed"), r
+        assert r["code"] == golhip.ERR_RCCL, r
+        assert r["seconds"] < timeout_ms / 1e3 + 15, r
+        msg = r["msg"]
+        assert f"rank {r['rank']} of 2" in msg and "end the process" in msg, msg
+        assert "golhip_comm_abort" in msg, msg
+        # the abort released the spinning RCCL kernels: the streams drained and the strips were
+        # freed within the deadline
+        assert r["drained"] and r["abort_close_seconds"] < timeout_ms / 1e3 + 10, r
+    # rank 0 waits for a halo that never comes: its error names the first incomplete RCCL
+    # operation -- an exchange, not merely the last operation queued (the count all-reduce)
+    assert "the first incomplete of" in res[0]["msg"], res[0]["msg"]
+    assert "halo exchange #" in res[0]["msg"] and "<- rank 1" in res[0]["msg"], res[0]["msg"]
+
+
 def test_stalled_rank_fails_at_the_deadline(golhip):
-    """GOLHIP_RING_SELF=2: every step's work ends in a 20 s stall of the compute stream (a rank
+    """GOLHIP_FAULT=stall: every step's work ends in a 20 s stall of the compute stream (a rank
     whose device work does not finish in time).  The sync polls against the 3 s deadline and
     returns ERR_RCCL at the deadline -- not after the stall -- naming the last exchange; the handle
-    refuses further work; destroy does not wait for the stalled stream.  Nothing RCCL is queued
-    behind the stall, and the communicator is not aborted after its set-up (an abort with RCCL
-    work queued behind a stall faulted the GPU: profiles/r04/r04d_failfast_abort_hooks.log)."""
+    refuses further work; destroy does not wait for the stalled stream."""
     timeout_ms = 3000
-    out = run_child("stall", timeout_ms, ring_self="2")
+    out = run_child("stall", timeout_ms, fault="stall")
     print(json.dumps(out))
     assert out.get("halo_rows") == 4, out
     assert not out.get("completed"), out

@@ -1,9 +1,15 @@
-"""The rank-mode ENGINE at world 2 and 3 on one GPU: golhip_create_rank_host runs the same engine as
-golhip_create_rank -- per-rank strips, the rank-independent launch plan, golhip_halo_plan's transfer
-order, the interior launch overlapped with the two boundary bands, the per-turn count reduction --
-with the halos and count sums carried by a gloo host transport instead of RCCL (RCCL refuses two
-ranks on one device, and the test box has one GPU).  Every rank's strip, every per-turn count, the
-alive-cell list and the per-turn flips must equal the single-board oracle.
+"""The rank-mode ENGINE at world 2 and 3 on one GPU, over both of its transports:
+  * "rccl": REAL RCCL ranks sharing this GPU -- a distinct NCCL_HOSTID per rank makes RCCL treat the
+    ranks as separate hosts (it refuses two ranks on one device otherwise: "Duplicate GPU") and
+    connect them through its network transport over loopback.  So ncclCommInitRankConfig with
+    several ranks, the grouped ncclSend/ncclRecv between ranks and the count ncclAllReduce run for
+    real -- what the driver's 8-GPU node runs, minus xGMI;
+  * "host": golhip_create_rank_host, the same engine with the halos and count sums carried by a
+    gloo host transport.
+Either way: per-rank strips, the rank-independent launch plan, golhip_halo_plan's transfer order,
+the interior launch overlapped with the two boundary bands, the per-turn count reduction.  Every
+rank's strip, every per-turn count, the alive-cell list and the per-turn flips must equal the
+single-board oracle.
 
 Reference analogue: broker/broker.go:37-56 (strip fan-out), :168-174 (stitch),
 gol/distributor.go:53-59,153-166 (flips, alive cells); the reference broadcasts the whole world to
@@ -35,21 +41,30 @@ def _free_port():
 SCHEDULE = [1, 7, 20, 33, 16, 3]  # K = 1 launches, tail plans, bulk depths, a short call
 
 
-def _worker(rank, world, port, width, height, k, out_dir):
+def _worker(rank, world, port, width, height, k, out_dir, transport="host"):
     for p in (str(ROOT / "oracle"), str(PKG)):
         if p not in sys.path:
             sys.path.insert(0, p)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if transport == "rccl":  # before anything initialises RCCL in this process
+        os.environ["NCCL_HOSTID"] = f"golhip-test-rank{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     import torch.distributed as dist
 
     import golhip
     import oracle
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    comm = golhip.GlooHostComm()
+    comm, nid = None, None
+    if transport == "host":
+        comm = golhip.GlooHostComm()
+    else:
+        obj = [golhip.nccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        nid = obj[0]
     res = {}
     with golhip.Engine(width, height, k=k, rank=rank, world_size=world, device=0,
-                       host_comm=comm) as e:
+                       host_comm=comm, nccl_id=nid) as e:
         y0, rows = e.info.y0, e.info.rows
         assert (y0, rows) == golhip.strip_bounds(height, world, rank)
         e.load_words(oracle.init_random(width, height, seed=11)[y0:y0 + rows])
@@ -71,21 +86,24 @@ def _worker(rank, world, port, width, height, k, out_dir):
             else np.zeros((0, 2), np.int32)
         res["flips_alive"] = alive
         res["words_end"] = e.store_words()
-    res["exchanges"] = np.array([comm.exchanges])
-    res["reduced"] = np.array(comm.reduced)
+    if comm is not None:
+        res["exchanges"] = np.array([comm.exchanges])
+        res["reduced"] = np.array(comm.reduced)
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **res)
     dist.barrier()
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("transport", ["rccl", "host"])
 @pytest.mark.parametrize("world,width,height,k", [
     (2, 1024, 1001, 16),   # uneven strips (500 / 501 rows)
     (3, 1024, 1000, 16),   # 333 / 333 / 334
     (2, 2048, 40, 16),     # strips shorter than 3k: the boundary launch waits for the halos
     (3, 576, 197, 8),      # width not a multiple of 128 (the torus is replicated horizontally)
+    (4, 1024, 403, 12),    # four ranks
 ])
-def test_rank_engine_host_transport_matches_oracle(tmp_path, oracle, world, width, height, k):
-    mp.start_processes(_worker, args=(world, _free_port(), width, height, k, str(tmp_path)),
+def test_rank_engine_matches_oracle(tmp_path, oracle, world, width, height, k, transport):
+    mp.start_processes(_worker, args=(world, _free_port(), width, height, k, str(tmp_path), transport),
                        nprocs=world, join=True, start_method="spawn")
     r = [dict(np.load(tmp_path / f"rank{i}.npz")) for i in range(world)]
     ref = oracle.init_random(width, height, seed=11)
@@ -119,10 +137,11 @@ def test_rank_engine_host_transport_matches_oracle(tmp_path, oracle, world, widt
         assert np.array_equal(np.concatenate(got), want), t
         prev = cur
     assert np.array_equal(np.concatenate([x["words_end"] for x in r]), ref)
-    # the transport really carried the exchanges: one per launch; count sums of every call
-    ex = [int(x["exchanges"][0]) for x in r]
-    assert len(set(ex)) == 1 and ex[0] >= len(SCHEDULE) + 5
-    assert all(np.array_equal(x["reduced"], r[0]["reduced"]) for x in r)
+    if transport == "host":
+        # the transport really carried the exchanges: one per launch; count sums of every call
+        ex = [int(x["exchanges"][0]) for x in r]
+        assert len(set(ex)) == 1 and ex[0] >= len(SCHEDULE) + 5
+        assert all(np.array_equal(x["reduced"], r[0]["reduced"]) for x in r)
 
 
 @pytest.mark.timeout(700)
@@ -147,6 +166,38 @@ def test_bench_rank_path_host_transport(tmp_path):
         assert line["parity"] is not None and line["parity"]["ok"], line["parity"]
         assert line["parity"]["cold_start_ok"]
         assert line["transport"].startswith("gloo host transport")
+
+
+@pytest.mark.timeout(400)
+def test_bench_rank_path_real_rccl_shared_gpu(tmp_path):
+    """bench.py --gpus 2 and 3 as torch.distributed.run launches it, every rank a REAL RCCL rank on
+    this one GPU (GOLHIP_RCCL_SHARED_GPU=1: distinct NCCL_HOSTIDs, RCCL's network transport): the
+    torch process group over RCCL, the engine's RCCL halo exchange and count all-reduce, the
+    shared-memory barrier and the per-rank block of the line.  The line's parity and board digest
+    (8192 x 8192*N, seed 3, oracle goldens at turn 25) must hold."""
+    for world in (2, 3):
+        env = dict(os.environ, GOLHIP_RCCL_SHARED_GPU="1", PYTHONUNBUFFERED="1")
+        env.pop("GOLHIP_HOST_COMM", None)
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={world}", "--master-addr", "127.0.0.1",
+               "--master-port", str(_free_port()), str(ROOT / "bench.py"), "--gpus", str(world),
+               "--size", "8192", "--steps", "20", "--warmup", "5", "--no-strong",
+               "--preheat-ms", "20", "--comm-timeout-ms", "60000"]
+        p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+        lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+        assert len(lines) == 1, p.stdout
+        line = json.loads(lines[0])
+        (tmp_path / f"bench_rccl_world{world}.json").write_text(lines[0])
+        print(lines[0][:2000])
+        assert line["n_gpus"] == world and line["config"]["height"] == 8192 * world
+        assert line["transport"].startswith("rccl, every rank on one GPU"), line["transport"]
+        assert line["process"]["process_group"] == "nccl", line["process"]
+        assert line["parity"] is not None and line["parity"]["ok"], line["parity"]
+        assert line["parity"]["cold_start_ok"] and line["parity"]["digest_ok"] is True, line["parity"]
+        pr = line["per_rank"]
+        assert [x["rank"] for x in pr] == list(range(world)), pr
+        assert all(x["split_blocks"] >= 1 and x["kernel_span_ms"] > 0 for x in pr), pr
 
 
 @pytest.mark.timeout(300)
