@@ -537,60 +537,90 @@ def configs_leg() -> dict:
     _, _, want = read_pgm_body(ref / "check" / "images" / "512x512x100.pgm")
     csv = [ln.split(",") for ln in (ref / "check" / "alive" / "512x512.csv").read_text().split()]
     want_counts = {int(t): int(c) for t, c in (r for r in csv if r[0].strip().isdigit())}
-    with golhip.Engine(w, h, k=16) as e:
-        e.load(board)
-        e.step(100, counts=True)  # warm (graphs, code paths)
-        runs = []
-        for _ in range(5):
+    def cfg1_runs(board_kernel: bool):
+        with golhip.Engine(w, h, k=16) as e:
+            e.set_board_kernel(board_kernel)
+            kind = e.launch_kind(16, counts=True)
             e.load(board)
-            e.sync()
-            t = time.perf_counter()
-            c = e.step(100, counts=True)
-            e.sync()
-            runs.append(time.perf_counter() - t)
-        out = e.store()
-    ok = (out.tobytes() == want and [int(x) for x in c] == [want_counts[t] for t in range(1, 101)])
-    dt = float(np.median(runs))
-    res["cfg1_512x100"] = {"us_per_turn": round(dt / 100 * 1e6, 3), "median_of": len(runs),
-                           "bit_exact_vs_reference_fixture": bool(ok)}
+            e.step(100, counts=True)  # warm (graphs, code paths)
+            runs = []
+            for _ in range(5):
+                e.load(board)
+                e.sync()
+                t = time.perf_counter()
+                c = e.step(100, counts=True)
+                e.sync()
+                runs.append(time.perf_counter() - t)
+            out = e.store()
+        ok = (out.tobytes() == want and [int(x) for x in c] == [want_counts[t] for t in range(1, 101)])
+        return float(np.median(runs)), ok, f"{kind[0]}{kind[1] or ''}"
+
+    dt, ok, kind = cfg1_runs(True)
+    dt_slab, ok_slab, kind_slab = cfg1_runs(False)
+    res["cfg1_512x100"] = {"us_per_turn": round(dt / 100 * 1e6, 3), "median_of": 5, "kernel": kind,
+                           "bit_exact_vs_reference_fixture": bool(ok and ok_slab),
+                           "multi_workgroup_slab": {"kernel": kind_slab,
+                                                    "us_per_turn": round(dt_slab / 100 * 1e6, 3)}}
     # configs[1]
     lines = (GOLDEN / gold["cfg2"]["counts_csv"]).read_text().split()[1:]
     exp2 = np.array([int(ln.split(",")[1]) for ln in lines], dtype=np.uint64)
-    with golhip.Engine(5120, 5120, k=16) as e:
-        kind = e.launch_kind(16, counts=True)
-        runs, ok = [], True
-        for _ in range(5):
-            e.init_random(2)
-            e.sync()
-            t = time.perf_counter()
-            c = e.step(10000, counts=True)
-            runs.append(time.perf_counter() - t)
-            ok = ok and bool(np.array_equal(c.astype(np.uint64), exp2))
-    runs_sorted = sorted(runs[1:])  # the first run captures the count graphs
+    def cfg2_runs(activity: bool):
+        with golhip.Engine(5120, 5120, k=16) as e:
+            e.set_activity(activity)
+            kind = e.launch_kind(16, counts=True)
+            runs, ok = [], True
+            for _ in range(5):
+                e.init_random(2)
+                e.sync()
+                t = time.perf_counter()
+                c = e.step(10000, counts=True)
+                runs.append(time.perf_counter() - t)
+                ok = ok and bool(np.array_equal(c.astype(np.uint64), exp2))
+            stats = e.activity_stats()
+        runs_sorted = sorted(runs[1:])  # the first run captures the count graphs
+        return runs, runs_sorted, ok, kind, stats
+
+    runs, runs_sorted, ok, kind, stats = cfg2_runs(True)
+    runs_d, runs_dsorted, ok_d, _, _ = cfg2_runs(False)
     dt = runs_sorted[len(runs_sorted) // 2]
+    dt_d = runs_dsorted[len(runs_dsorted) // 2]
     res["cfg2_5120x10000"] = {"us_per_turn": round(dt / 10000 * 1e6, 3),
                               "best_us_per_turn": round(runs_sorted[0] / 10000 * 1e6, 3),
                               "runs_s": [round(r, 4) for r in runs],
                               "gcups": round(5120 * 5120 * 10000 / dt / 1e9, 1),
-                              "counts_match_all_10000": ok, "kernel": f"{kind[0]}{kind[1] or ''}"}
+                              "counts_match_all_10000": bool(ok and ok_d), "kernel": f"{kind[0]}{kind[1] or ''}",
+                              "stable_slab_skipping": {"slabs_computed": stats[0], "slabs_skipped": stats[1]},
+                              "without_skipping": {"us_per_turn": round(dt_d / 10000 * 1e6, 3),
+                                                   "gcups": round(5120 * 5120 * 10000 / dt_d / 1e9, 1)}}
     # configs[4]
     b = np.zeros((4096, 4096), dtype=np.uint8)
     golhip.place(b, golhip.parse_rle((GOLDEN / "gosper_gun.rle").read_text()), 64, 64)
     golhip.place(b, golhip.parse_rle((GOLDEN / "r_pentomino.rle").read_text()), 2048, 2048)
     deltas = np.load(GOLDEN / gold["cfg5"]["counts_1e6_npz"])["deltas"]
     exp5 = (int((b == 255).sum()) + np.cumsum(deltas.astype(np.int64))).astype(np.uint64)
-    with golhip.Engine(4096, 4096, k=16) as e:
-        kind = e.launch_kind(16, counts=True)
-        e.load(b)
-        e.step(4096, counts=True)  # capture the count graphs
-        e.load(b)
-        e.sync()
-        t = time.perf_counter()
-        c = e.step(1000000, counts=True)
-        dt = time.perf_counter() - t
+    def cfg5_run(activity: bool):
+        with golhip.Engine(4096, 4096, k=16) as e:
+            e.set_activity(activity)
+            kind = e.launch_kind(16, counts=True)
+            e.load(b)
+            e.step(4096, counts=True)  # capture the count graphs
+            e.load(b)
+            e.sync()
+            s0 = e.activity_stats()
+            t = time.perf_counter()
+            c = e.step(1000000, counts=True)
+            dt = time.perf_counter() - t
+            s1 = e.activity_stats()
+        return dt, bool(np.array_equal(c.astype(np.uint64), exp5)), kind, (s1[0] - s0[0], s1[1] - s0[1])
+
+    dt, ok5, kind, stats = cfg5_run(True)
+    dt_d, ok5_d, _, _ = cfg5_run(False)
     res["cfg5_4096x1e6"] = {"us_per_turn": round(dt, 3), "gcups": round(4096 * 4096 * 1e6 / dt / 1e9, 1),
-                            "counts_match_all_1e6": bool(np.array_equal(c.astype(np.uint64), exp5)),
-                            "kernel": f"{kind[0]}{kind[1] or ''}"}
+                            "counts_match_all_1e6": bool(ok5 and ok5_d),
+                            "kernel": f"{kind[0]}{kind[1] or ''}",
+                            "stable_slab_skipping": {"slabs_computed": stats[0], "slabs_skipped": stats[1]},
+                            "without_skipping": {"us_per_turn": round(dt_d, 3),
+                                                 "gcups": round(4096 * 4096 * 1e6 / dt_d / 1e9, 1)}}
     res["ok"] = bool(res["cfg1_512x100"]["bit_exact_vs_reference_fixture"]
                      and res["cfg2_5120x10000"]["counts_match_all_10000"]
                      and res["cfg5_4096x1e6"]["counts_match_all_1e6"])

@@ -113,6 +113,7 @@ void board_replaced(golhip_t h) {
     h->turn = 0;
     h->prev_valid = false;
     h->diff_valid = false;
+    h->act_valid = false;  // the stable-slab flags describe the old board
 }
 
 }  // namespace
@@ -292,6 +293,7 @@ int golhip_checkpoint_load(golhip_t h, const char *path) {
     h->turn = hd.turn;
     h->prev_valid = false;
     h->diff_valid = false;
+    h->act_valid = false;
     return GOLHIP_OK;
 }
 

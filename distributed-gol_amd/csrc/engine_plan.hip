@@ -308,6 +308,13 @@ RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K, bool counting) 
     return rk;
 }
 
+bool board_applies(golhip_t h, int *W, int *R) {
+    // the production kernel family only, and no forced kernel or band (tests, tuning)
+    if (!h->board_kernel || h->split || h->shards.size() != 1 || h->variant != kVariantProd) return false;
+    if (h->force_split > 0 || h->force_tile >= 0 || h->force_slab >= 0 || h->band_rows > 0) return false;
+    return stencil_board_shape(h->height, h->wd, W, R);
+}
+
 // Largest band the kernels' 32-bit store offsets can address: a band's output descriptor spans
 // band * rowbytes bytes, and dropped stores use offset kOutOfRange (2^30) + row * rowbytes, so
 // band * rowbytes must stay below 2^30 (golhip_kernels.hip, buffer_store_words).  At 262144 wide
@@ -319,20 +326,68 @@ static int64_t max_band_rows(golhip_t h) {
 
 // Launch the K-generation stencil described by p (the register kernels or the level-split kernel
 // when the board asks for them).
+// Stable-slab skipping applies to a slab launch when: enabled, a production gol_slab2 shape, no flips,
+// the whole torus in one strip (bands wrap), and every band at least K rows tall (the 3 x 3 slabs
+// around a slab then cover the radius-K region its next K generations depend on).
+static bool activity_applies(golhip_t h, const RegKernel &rk, const StencilParams &q, int K) {
+    if (!h->activity || h->split || q.diff || q.diff_stride > 0 || q.r1e > q.r1b || q.wrap_rows <= 0) return false;
+    if (rk.kind != 3 || !stencil_slab_activity(K, rk.W, rk.S, rk.NC)) return false;
+    const int64_t rows = q.r0e - q.r0b, last = rows - (q.nbands - 1) * q.band;
+    return q.r0b == 0 && rows == q.wrap_rows && (q.nbands == 1 || last >= K);
+}
+
+// the slab launch's params (band = T rows, one slab per band and 62-word chunk)
+static StencilParams slab_params(golhip_t h, const StencilParams &p, int T) {
+    StencilParams q = p;
+    q.band = T;
+    q.band2 = q.nbig0 = 0;
+    q.nbands0 = (p.r0e - p.r0b + T - 1) / T;
+    q.nbands = q.nbands0 + (p.r1e - p.r1b + T - 1) / T;
+    q.nchunks = (int32_t)((h->wd + kTileChunkWords - 1) / kTileChunkWords);
+    return q;
+}
+
+int ensure_activity(golhip_t h, Shard &s, int K, bool counting) {
+    const RegKernel rk = pick_reg_kernel(h, s.rows, K, counting);
+    if (!rk.kind || !h->activity) return GOLHIP_OK;
+    const StencilParams q = slab_params(h, make_params(h, s, K, 0, s.rows, 0, 0, 0, counting), rk.out_rows());
+    const int64_t need = q.nbands * (int64_t)q.nchunks;
+    if (!activity_applies(h, rk, q, K) || need <= s.act_cap) return GOLHIP_OK;
+    HIPCHK(h, hipSetDevice(s.device));
+    SYNCCHK(h, s.compute);
+    if (s.act) HIPCHK(h, hipFree(s.act));
+    s.act = nullptr;
+    s.act_cap = 0;
+    HIPCHK(h, hipMalloc(&s.act, sizeof(uint32_t) * 4 * (size_t)need));
+    if (!s.act_stats) {
+        HIPCHK(h, hipMalloc(&s.act_stats, sizeof(unsigned long long) * 2));
+        HIPCHK(h, hipMemsetAsync(s.act_stats, 0, sizeof(unsigned long long) * 2, s.compute));
+    }
+    s.act_cap = need;
+    h->act_valid = false;
+    return GOLHIP_OK;
+}
+
 hipError_t launch_auto(golhip_t h, int K, const uint32_t *in, uint32_t *out, const StencilParams &p,
-                       unsigned long long *slots, hipStream_t s) {
+                       unsigned long long *slots, hipStream_t s, Shard *sh, int par, bool act_reset_first) {
     const int64_t rows_total = (p.r0e - p.r0b) + (p.r1e - p.r1b);
     if (const RegKernel rk = pick_reg_kernel(h, rows_total, K, slots != nullptr); rk.kind) {
-        StencilParams q = p;
-        const int T = rk.out_rows();
-        q.band = T;
-        q.band2 = q.nbig0 = 0;
-        q.nbands0 = (p.r0e - p.r0b + T - 1) / T;
-        q.nbands = q.nbands0 + (p.r1e - p.r1b + T - 1) / T;
-        q.nchunks = (int32_t)((h->wd + kTileChunkWords - 1) / kTileChunkWords);
-        return rk.kind == 2 ? launch_stencil_tile(K, T, in, out, q, slots, s)
+        StencilParams q = slab_params(h, p, rk.out_rows());
+        const int64_t key[3] = {rk.out_rows(), q.nbands, q.nchunks};
+        if (sh && sh->act && activity_applies(h, rk, q, K) && q.nbands * (int64_t)q.nchunks <= sh->act_cap) {
+            q.act = sh->act;
+            q.act_stats = sh->act_stats;
+            q.act_par = par;
+            q.act_reset = act_reset_first || !h->act_valid || !std::equal(key, key + 3, h->act_key);
+            h->act_valid = true;
+            std::copy(key, key + 3, h->act_key);
+        } else {
+            h->act_valid = false;
+        }
+        return rk.kind == 2 ? launch_stencil_tile(K, q.band, in, out, q, slots, s)
                             : launch_stencil_slab(K, rk.W, rk.S, rk.NC, in, out, q, slots, s);
     }
+    h->act_valid = false;
     const int S = pick_split(h, rows_total, K);
     if (S > 1) {
         // the level-split kernel has its own column geometry (half-word halo for K <= 16)
@@ -427,6 +482,11 @@ int golhip_launch_kind_counts(golhip_t h, int k, int counting, int *kind, int *p
     *kind = 0;
     *param = 0;
     if (h->split) return GOLHIP_OK;  // strips: the streaming kernel around the halo exchange
+    if (int W = 0, R = 0; board_applies(h, &W, &R)) {  // the whole board in one workgroup
+        *kind = 4;
+        *param = W * 100 + R;
+        return GOLHIP_OK;
+    }
     const int64_t rows = h->shards[0].rows;
     if (const RegKernel rk = pick_reg_kernel(h, rows, k, counting != 0); rk.kind) {
         *kind = rk.kind;
@@ -454,9 +514,18 @@ int golhip_launch_plan(int64_t width, int64_t height, int strips, int k, int64_t
     const bool stream = strips > 1 ||
                         !stencil_slab_supported(Kfull, 8, Kfull == 16 ? 12 : 8, Kfull == 16 ? 9 : 4) ||
                         waves1 > kSlabMaxWaves1PerCu * 256;
+    size_t cnt = 0;
+    if (strips == 1 && stencil_board_shape(height, (int32_t)wd, nullptr, nullptr)) {
+        // the whole-board kernel: one launch per kBoardMaxK generations (of the count window)
+        for (int64_t left = turns; left > 0; left -= kBoardMaxK) {
+            if (depths && cnt < cap) depths[cnt] = (int32_t)std::min<int64_t>(left, kBoardMaxK);
+            ++cnt;
+        }
+        *n = cnt;
+        return cnt > cap && depths ? GOLHIP_ERR_CAP : GOLHIP_OK;
+    }
     LaunchPlanner plan(strip_cells, k, turns, strips == 1 && small_board(cells, Kfull), false, false,
                        4096, stream);
-    size_t cnt = 0;
     while (plan.left > 0) {
         const int K = plan.next();
         if (depths && cnt < cap) depths[cnt] = K == 0 ? -(plan.last_M * plan.Kfull) : K;

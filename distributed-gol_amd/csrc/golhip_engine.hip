@@ -131,7 +131,8 @@ void free_shard(Shard &s, int64_t drain_ms, bool comm_failed) {
     if (s.dev_counts) (void)hipFree(s.dev_counts);
     if (s.pin_counts) (void)hipHostFree(s.pin_counts);
     for (void *q : {(void *)s.diffbuf, (void *)s.ring, (void *)s.ex_rowcounts, (void *)s.ex_offsets,
-                    (void *)s.ex_slot_counts, (void *)s.ex_xy, (void *)s.stage, (void *)s.ex_block_sums})
+                    (void *)s.ex_slot_counts, (void *)s.ex_xy, (void *)s.stage, (void *)s.ex_block_sums,
+                    (void *)s.act, (void *)s.act_stats})
         if (q) (void)hipFree(q);
     if (s.ev_ready) (void)hipEventDestroy(s.ev_ready);
     if (s.ev_halo) (void)hipEventDestroy(s.ev_halo);
@@ -296,8 +297,13 @@ int step_block(golhip_t h, int K, int64_t slot_gen, int64_t diff_slot = kDiffNon
             // a K-deep ring launch (ring_depth: a production register slab) writes the flips of
             // each of its K generations into K consecutive ring slots
             p.diff_stride = diff_slot >= 0 && K > 1 ? s.rows * h->pitch : 0;
-            HIPCHK(h, launch_auto(h, K, in, out, p, slots, s.compute));
+            if (!diff) {  // stable-slab skipping: its flags (allocated here, outside any capture)
+                int rc = ensure_activity(h, s, K, slots != nullptr);
+                if (rc) return rc;
+            }
+            HIPCHK(h, launch_auto(h, K, in, out, p, slots, s.compute, &s, h->cur));
         } else if (s.rows >= 3 * K) {
+            h->act_valid = false;
             // The interior rows need no halo: they run while the halos are exchanged.  The two
             // boundary bands wait for the halos on their own stream and run concurrently with the
             // interior, in wave slots the interior launch leaves free for them; the compute stream
@@ -334,6 +340,7 @@ int step_block(golhip_t h, int K, int64_t slot_gen, int64_t diff_slot = kDiffNon
             if (tp) HIPCHK(h, hipEventRecord(tp->b, s.compute));
             h->edge_k = K;
         } else {
+            h->act_valid = false;
             h->edge_k = 0;
             HIPCHK(h, hipStreamWaitEvent(s.compute, s.ev_halo, 0));
             StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0, 0, slots != nullptr);
@@ -353,6 +360,34 @@ int step_block(golhip_t h, int K, int64_t slot_gen, int64_t diff_slot = kDiffNon
     h->turn += K;
     h->prev_valid = (K == 1);
     h->diff_valid = diff_slot == kDiffLast;
+    return GOLHIP_OK;
+}
+
+// One K-generation launch of the whole-board kernel (stencil_board.hip): the step_block of boards
+// that fit one workgroup.  slot_gen / diff_slot as step_block's (no flips ring).
+int board_block(golhip_t h, int K, int W, int R, int64_t slot_gen, int64_t diff_slot) {
+    Shard &s = h->shards[0];
+    HIPCHK(h, hipSetDevice(s.device));
+    StencilParams p{};
+    p.pitch = h->pitch;
+    p.wd = h->wd;
+    p.r0e = s.rows;
+    p.wrap_rows = h->height;
+    p.hi = s.rows;
+    p.nchunks = 1;
+    p.diff = diff_slot == kDiffLast ? s.diffbuf : nullptr;
+    unsigned long long *slots = slot_gen >= 0 ? s.slots + slot_gen * kCountSlots : nullptr;
+    HIPCHK(h, launch_stencil_board(K, W, R, h->row0(s, h->cur), h->row0(s, h->cur ^ 1), p, slots, s.compute));
+    if (h->timing) {
+        h->tlaunches += 1;
+        h->tgens += K;
+    }
+    h->queued_s += (double)h->L * (double)h->height * K / 5e10 + kLaunchOverheadUs * 1e-6;
+    h->cur ^= 1;
+    h->turn += K;
+    h->prev_valid = (K == 1);
+    h->diff_valid = diff_slot == kDiffLast;
+    h->act_valid = false;
     return GOLHIP_OK;
 }
 
@@ -396,9 +431,15 @@ int graph_for(golhip_t h, int K, int M, bool counting, hipGraphExec_t *out) {
         if (g.K == K && g.M == M && g.cur == h->cur && g.counting == counting && g.band == band &&
             g.tail_bands == h->tail_bands && g.tail_rows == h->tail_rows) {
             *out = g.exec;
+            h->act_valid = g.act_after;  // the flags as the replay leaves them
+            std::copy(g.act_key_after, g.act_key_after + 3, h->act_key);
             return GOLHIP_OK;
         }
     HIPCHK(h, hipSetDevice(s.device));
+    {
+        int rc = ensure_activity(h, s, K, counting);
+        if (rc) return rc;
+    }
     if (counting && !h->g_counts) HIPCHK(h, hipMalloc(&h->g_counts, sizeof(unsigned long long) * kGraphGensBig * 2));
     hipGraph_t graph = nullptr;
     HIPCHK(h, hipStreamBeginCapture(s.compute, hipStreamCaptureModeThreadLocal));
@@ -406,8 +447,11 @@ int graph_for(golhip_t h, int K, int M, bool counting, hipGraphExec_t *out) {
     for (int i = 0; i < M && err == hipSuccess; ++i) {
         const int c = h->cur ^ (i & 1);
         StencilParams p = make_params(h, s, K, 0, s.rows, 0, 0, 0, counting);
+        // the first launch of a replay recomputes the stable-slab flags (a replay must not trust
+        // flags another state left)
         err = launch_auto(h, K, h->row0(s, c), h->row0(s, c ^ 1), p,
-                          counting ? s.slots + (int64_t)i * K * kCountSlots : nullptr, s.compute);
+                          counting ? s.slots + (int64_t)i * K * kCountSlots : nullptr, s.compute, &s, c,
+                          i == 0);
     }
     if (err == hipSuccess && counting)  // one finalize for the graph's M*K generations
         err = launch_count_finalize(M * K, s.slots, h->g_counts, s.compute);
@@ -422,6 +466,8 @@ int graph_for(golhip_t h, int K, int M, bool counting, hipGraphExec_t *out) {
     g.band = band;
     g.tail_bands = h->tail_bands;
     g.tail_rows = h->tail_rows;
+    g.act_after = h->act_valid;
+    std::copy(h->act_key, h->act_key + 3, g.act_key_after);
     err = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
     (void)hipGraphDestroy(graph);
     if (err != hipSuccess) return fail(h, GOLHIP_ERR_HIP, "graph instantiate: %s", hipGetErrorString(err));
@@ -442,6 +488,8 @@ int run_steps(golhip_t h, int64_t turns, uint64_t *alive_per_turn, bool ring) {
         return fail(h, GOLHIP_ERR_STATE, "flips need a production kernel variant (tuning variant %d cannot write them)",
                     h->variant);
     const bool counting = alive_per_turn != nullptr;
+    int bw = 0, br = 0;  // the whole-board kernel: W waves x R rows per segment
+    const bool board = !ring && board_applies(h, &bw, &br);
     const int kmax = pick_k(h->k);
     const bool stream = !ring && h->shards.size() == 1 &&
                         pick_reg_kernel(h, h->shards[0].rows, kmax, counting).kind == 0 &&
@@ -453,8 +501,9 @@ int run_steps(golhip_t h, int64_t turns, uint64_t *alive_per_turn, bool ring) {
     if (counting) {
         // pinned host counts for calls that replay no graph (their graph replays would copy each
         // replay's counts into it); the others keep the device buffer and one copy returns them
-        const bool host_counts =
-            h->shards.size() == 1 && !rccl_waits(h) && turns <= kPinnedCountTurns && !plan.replays();
+        // (the whole-board kernel replays no graph: one finalize per count window writes them)
+        const bool host_counts = h->shards.size() == 1 && !rccl_waits(h) &&
+                                 (board || (turns <= kPinnedCountTurns && !plan.replays()));
         for (auto &s : h->shards) {
             unsigned long long *&buf = host_counts ? s.pin_counts : s.dev_counts;
             size_t &cap = host_counts ? s.pin_counts_cap : s.dev_counts_cap;
@@ -487,6 +536,21 @@ int run_steps(golhip_t h, int64_t turns, uint64_t *alive_per_turn, bool ring) {
     const int Kfull = plan.Kfull;
     int64_t win = 0;  // generations pending in the count window, from turn offset done - win
     while (done < turns) {
+        if (board) {  // one launch per count window (or kBoardMaxK generations)
+            if (counting && win >= h->count_window) {
+                int rc = flush_counts_window(h, (int)win, done - win);
+                if (rc) return rc;
+                win = 0;
+            }
+            int64_t K = std::min<int64_t>(turns - done, kBoardMaxK);
+            if (counting) K = std::min<int64_t>(K, h->count_window - win);
+            const int64_t diff_slot = h->track_flips && done + K == turns ? kDiffLast : kDiffNone;
+            int rc = board_block(h, (int)K, bw, br, counting ? win : -1, diff_slot);
+            if (rc) return rc;
+            done += K;
+            if (counting) win += K;
+            continue;
+        }
         const int K = ring ? ring_depth(h, turns - done, counting) : plan.next();
         if (K == 0) {  // one graph replay of M x Kfull generations
             const int M = plan.last_M;
@@ -787,6 +851,36 @@ int golhip_edge_wait(golhip_t h, double *total_ms, int64_t *blocks) {
     if (rc) return rc;
     if (total_ms) *total_ms = h->tedge_ms;
     if (blocks) *blocks = h->tedge_blocks;
+    return GOLHIP_OK;
+}
+
+int golhip_set_activity(golhip_t h, int enable) {
+    if (!h) return GOLHIP_ERR_ARG;
+    h->activity = enable != 0;
+    h->act_valid = false;
+    return GOLHIP_OK;
+}
+
+int golhip_activity_stats(golhip_t h, int64_t *computed, int64_t *skipped) {
+    if (!h) return GOLHIP_ERR_ARG;
+    int rc = sync_all(h);
+    if (rc) return rc;
+    unsigned long long v[2] = {0, 0};
+    for (auto &s : h->shards)
+        if (s.act_stats) {
+            unsigned long long t[2];
+            HIPCHK(h, hipSetDevice(s.device));
+            HIPCHK(h, hipMemcpy(t, s.act_stats, sizeof t, hipMemcpyDeviceToHost));
+            v[0] += t[0], v[1] += t[1];
+        }
+    if (computed) *computed = (int64_t)v[0];
+    if (skipped) *skipped = (int64_t)v[1];
+    return GOLHIP_OK;
+}
+
+int golhip_set_board_kernel(golhip_t h, int enable) {
+    if (!h) return GOLHIP_ERR_ARG;
+    h->board_kernel = enable != 0;
     return GOLHIP_OK;
 }
 

@@ -103,6 +103,10 @@ struct Shard {
     // synchronises the whole device, and every `s` snapshot / PGM store used to pay one)
     uint8_t *stage = nullptr;
     int64_t stage_bytes = 0;
+    // stable-slab skipping (StencilParams::act): 4 x act_cap uint32 flags, 2 uint64 counters
+    uint32_t *act = nullptr;
+    int64_t act_cap = 0;
+    unsigned long long *act_stats = nullptr;
 };
 
 struct TimingPair {
@@ -117,6 +121,10 @@ struct GraphEntry {
     bool counting = false;
     int64_t band = 0;
     int tail_bands = 0, tail_rows = 0;  // golhip_set_tail_bands at capture
+    // stable-slab skipping: a graph's first launch always recomputes its flags (act_reset), so a
+    // replay never trusts flags of another state; after it the flags are those of its geometry
+    bool act_after = false;
+    int64_t act_key_after[3] = {0, 0, 0};
     hipGraphExec_t exec = nullptr;
 };
 
@@ -159,6 +167,13 @@ struct golhip_engine {
     // the boundary bands' waves raise their issue priority (StencilParams::prio)
     int edge_setprio = 1;
     int graph_mode = -1;  // golhip_set_graphs: -1 automatic, 0 never, 1 whenever the plan allows
+    // stable-slab skipping (golhip_set_activity; on by default): the slab flags on the shard hold
+    // the state of the last launch when act_valid, for slab geometry act_key (T, nbands, nchunks)
+    bool activity = true;
+    bool act_valid = false;
+    // the whole-board kernel for the boards it fits (golhip_set_board_kernel; on by default)
+    bool board_kernel = true;
+    int64_t act_key[3] = {0, 0, 0};
     // RCCL fail-fast (rank mode): every host wait on work that can depend on an RCCL transfer polls
     // ncclCommGetAsyncError against a deadline and fails the handle when it passes
     // (golhip_set_comm_timeout); the communicator is non-blocking, so no RCCL call blocks the host
@@ -305,8 +320,15 @@ struct RegKernel {
     int out_rows() const { return T; }  // output rows per tile / slab
 };
 RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K, bool counting);
+// sh (nullable): the shard launched on, for stable-slab skipping of its slab launches; par: the
+// input buffer's parity (the slab flags' parity); act_reset_first: recompute the flags even if they
+// look valid (a captured graph's first launch)
 hipError_t launch_auto(golhip_t h, int K, const uint32_t *in, uint32_t *out, const StencilParams &p,
-                       unsigned long long *slots, hipStream_t s);
+                       unsigned long long *slots, hipStream_t s, Shard *sh = nullptr, int par = 0,
+                       bool act_reset_first = false);
+// The flag arrays a K-deep launch of this single-strip board needs for stable-slab skipping
+// (allocated outside any graph capture); GOLHIP_OK when none are needed.
+int ensure_activity(golhip_t h, Shard &s, int K, bool counting);
 StencilParams make_params(golhip_t h, const Shard &s, int K, int64_t r0b, int64_t r0e, int64_t r1b,
                           int64_t r1e, int64_t reserve_waves = 0, bool counting = false);
 bool small_board(double cells, int K);
@@ -332,6 +354,10 @@ struct LaunchPlanner {
 // Kernel variants whose launches can write a generation's flips beside their output.
 bool variant_writes_flips(int v);
 int ensure_extract_scratch(golhip_t h, Shard &s, int64_t rows, int64_t slots);
+
+// Whether golhip_step runs this single-strip board with the whole-board kernel (stencil_board.hip),
+// and its shape.
+bool board_applies(golhip_t h, int *W = nullptr, int *R = nullptr);
 
 // ---- golhip_engine.hip: the step loop -----------------------------------------------------------
 int run_steps(golhip_t h, int64_t turns, uint64_t *alive_per_turn, bool ring);

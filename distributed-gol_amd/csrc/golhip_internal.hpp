@@ -55,6 +55,16 @@ struct StencilParams {
     // null in production; the tuning library's stamp handles: gol_slab2's per-wave phase stamps,
     // 8 uint64 per wave (golhip_tuning_stamps_ex, scripts/slab_stamps.py)
     uint64_t *stamp;
+    // Stable-slab skipping (gol_slab2 ACT, single-strip torus boards; null: off).  act holds four
+    // arrays of nbands * nchunks uint32, one entry per slab (workgroup): changed[0], changed[1] (did
+    // the slab's output change in the last generation of the launch that wrote it; this launch reads
+    // changed[act_par] and writes changed[act_par ^ 1]), same (both ping-pong buffers hold the slab's
+    // output region identically) and pop (its alive cells at that last generation).  act_reset: the
+    // flags are stale (a new board, another kernel ran): every slab computes and rewrites them.
+    // act_stats (nullable): two uint64 counters, slabs computed / slabs skipped.
+    uint32_t *act;
+    unsigned long long *act_stats;
+    int32_t act_par, act_reset;
 };
 
 constexpr int kMaxK = 32;         // generations per launch limit (halo lane = 32 bits)
@@ -201,7 +211,17 @@ bool stencil_slab_supported(int K, int W, int S, int NC = 4);
 // the slab shapes that can write EVERY generation's flips (StencilParams::diff_stride > 0): the
 // production shapes pick_reg_kernel chooses
 bool stencil_slab_flips_every_gen(int K, int W, int S, int NC = 4);
+// the slab shapes whose launches can skip stable slabs (StencilParams::act): the production gol_slab2
+// shapes, without flips
+bool stencil_slab_activity(int K, int W, int S, int NC);
 hipError_t warm_stencil_tile(hipStream_t s);
+// The whole-board kernel (stencil_board.hip): one workgroup holds a board of wd in {4, 8, 16} words
+// and `height` = 4 W R rows in registers and runs K (runtime, <= kBoardMaxK) generations in one
+// launch.  stencil_board_shape: whether the board fits, and its (W waves, R rows per segment).
+constexpr int kBoardMaxK = 4096;
+bool stencil_board_shape(int64_t height, int32_t wd, int *W, int *R);
+hipError_t launch_stencil_board(int K, int W, int R, const uint32_t *in_row0, uint32_t *out_row0,
+                                const StencilParams &p, unsigned long long *slots, hipStream_t s);
 constexpr int kTileChunkWords = 62;
 // Words per column chunk of the level-split kernel (half-word halo for K <= 16).
 __host__ __device__ constexpr int split_chunk_words(int K) { return K <= 16 ? 63 : 62; }

@@ -30,6 +30,10 @@ bool stencil_slab_flips_every_gen(int K, int W, int S, int NC) {
     return stencil_slab_supported(K, W, S, NC) && slab_prod_shape(K, W, S, NC);
 }
 
+bool stencil_slab_activity(int K, int W, int S, int NC) {
+    return slab_prod_supported(K, W, S, NC) && (NC == kSlab2 || NC == kSlab2E);
+}
+
 bool stencil_slab_supported(int K, int W, int S, int NC) {
     if (slab_prod_supported(K, W, S, NC)) return true;
     const auto f = kernel_extras().slab_supported;

@@ -39,7 +39,8 @@ EXPORTS = [
     "golhip_version", "golhip_strerror", "golhip_device_count", "golhip_strip_bounds",
     "golhip_halo_plan",
     "golhip_create", "golhip_create_strips", "golhip_nccl_unique_id", "golhip_create_rank",
-    "golhip_comm_abort", "golhip_edge_wait",
+    "golhip_comm_abort", "golhip_edge_wait", "golhip_set_activity", "golhip_activity_stats",
+    "golhip_set_board_kernel",
     "golhip_create_rank_host", "golhip_destroy",
     "golhip_last_error", "golhip_get_info", "golhip_load_bytes", "golhip_init_random",
     "golhip_store_bytes", "golhip_store_words", "golhip_load_words", "golhip_step",
@@ -206,6 +207,9 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
         "golhip_timing": ([H, i32], i32),
         "golhip_kernel_time": ([H, ctypes.POINTER(ctypes.c_double), i64p, i64p], i32),
         "golhip_edge_wait": ([H, ctypes.POINTER(ctypes.c_double), i64p], i32),
+        "golhip_set_activity": ([H, i32], i32),
+        "golhip_set_board_kernel": ([H, i32], i32),
+        "golhip_activity_stats": ([H, i64p, i64p], i32),
         "golhip_launch_plan": ([i64, i64, i32, i32, i64, ctypes.c_void_p, ctypes.c_size_t,
                                 ctypes.POINTER(ctypes.c_size_t)], i32),
         "golhip_launch_kind": ([H, i32, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], i32),
@@ -601,17 +605,31 @@ class Engine:
 
     def launch_kind(self, k: int, counts: bool = False) -> tuple[str, int]:
         """The kernel a k-deep launch runs (with / without per-generation counts): ("stream", 0),
-        ("split", S), ("tile", T) or ("slab", [10000 NC +] 100 W + S)."""
+        ("split", S), ("tile", T), ("slab", [10000 NC +] 100 W + S) or ("board", 100 W + R)."""
         kind, param = ctypes.c_int(), ctypes.c_int()
         self._check(self._L.golhip_launch_kind_counts(self._h, k, int(counts), ctypes.byref(kind),
                                                       ctypes.byref(param)))
-        return ("stream", "split", "tile", "slab")[kind.value], param.value
+        return ("stream", "split", "tile", "slab", "board")[kind.value], param.value
 
     def sync(self):
         self._check(self._L.golhip_sync(self._h))
 
     def timing(self, enable: bool):
         self._check(self._L.golhip_timing(self._h, int(enable)))
+
+    def set_activity(self, enable: bool):
+        """Stable-slab skipping of the small-board slab launches (golhip_set_activity; default on)."""
+        self._check(self._L.golhip_set_activity(self._h, int(enable)))
+
+    def set_board_kernel(self, enable: bool):
+        """The whole-board kernel for boards that fit one workgroup (golhip_set_board_kernel)."""
+        self._check(self._L.golhip_set_board_kernel(self._h, int(enable)))
+
+    def activity_stats(self) -> tuple[int, int]:
+        """(slabs computed, slabs skipped) since create (golhip_activity_stats)."""
+        c, k = ctypes.c_int64(), ctypes.c_int64()
+        self._check(self._L.golhip_activity_stats(self._h, ctypes.byref(c), ctypes.byref(k)))
+        return c.value, k.value
 
     def edge_wait(self) -> tuple[float, int]:
         """With timing on (split boards): ms the compute stream waited for the boundary bands after

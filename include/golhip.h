@@ -225,7 +225,8 @@ int golhip_set_tail_bands(golhip_t h, int bands, int rows);
 /* Which kernel a k-deep launch on this handle's first strip runs: *kind = 0 the streaming kernel
  * (gol_stencil, gol_step1 at k = 1), 1 the level-split kernel (*param = waves per band), 2 the
  * register-tile kernel gol_tile (*param = tile height T), 3 the register-slab kernel gol_slab
- * (*param = [10000 * row chains +] 100 * waves + rows per wave).  Introspection for tests and the
+ * (*param = [10000 * row chains +] 100 * waves + rows per wave), 4 the whole-board kernel gol_board
+ * (*param = 100 * waves + rows per segment; golhip_set_board_kernel).  Introspection for tests and the
  * bench line.  golhip_launch_kind describes a launch without per-generation counts,
  * golhip_launch_kind_counts one with (counting != 0) or without them: small boards pick a
  * different slab shape when counting. */
@@ -254,6 +255,22 @@ int golhip_set_comm_timeout(golhip_t h, int64_t ms);
  * GOLHIP_ERR_STATE if the communicator has not failed. */
 int golhip_comm_abort(golhip_t h);
 int golhip_sync(golhip_t h);                         /* wait for all queued device work */
+/* The whole-board kernel (default on): a single-strip board of 128, 256 or 512 torus cells per row
+ * (any width up to 512 whose lcm with 128 is one of them: the reference's 16/64/128/256/512 sizes)
+ * and 4 W R rows (4 ... 512) runs in ONE workgroup holding the whole torus in registers, every
+ * golhip_step call as one launch per 4096 generations: no temporal-blocking trapezoid, no halo
+ * lanes, no launch boundary inside a call.  enable = 0 keeps the multi-workgroup slab kernels
+ * (A/B).  golhip_launch_kind reports it as kind 4 (*param = 100 * waves + rows per segment). */
+int golhip_set_board_kernel(golhip_t h, int enable);
+/* Stable-slab skipping (default on): the register-slab launches of single-strip small boards skip
+ * every slab whose neighbourhood did not change in the previous launch's last generation -- Life's
+ * radius-1 rule keeps such a slab fixed for the launch's K generations -- copying it once and
+ * counting its cached alive cells for each generation.  Results are identical either way (a settled
+ * board, e.g. configs[4] after ~70 000 turns, skips nearly every slab).  enable = 0 computes every
+ * slab (A/B, dense-equivalent timing). */
+int golhip_set_activity(golhip_t h, int enable);
+/* Slab launches computed / skipped on this handle since it was created (stable-slab skipping). */
+int golhip_activity_stats(golhip_t h, int64_t *computed, int64_t *skipped);
 /* HIP-event timing of golhip_step calls on the handle's first strip (one event pair per call
  * around its back-to-back stencil launches); kernel_time reports the summed span, the number of
  * stencil launch blocks and generations. */

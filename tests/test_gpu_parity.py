@@ -170,7 +170,8 @@ def test_step_flips_sdl_512_every_count(golhip, oracle):
     shadow = (board == 255)
     with golhip.Engine(512, 512, k=16) as e:
         e.load(board)
-        assert e.launch_kind(16)[0] == "slab"
+        # golhip_step runs this board with the whole-board kernel; the flips ring with slabs
+        assert e.launch_kind(16)[0] == "board"
         t0 = 0
         for turns in (64, 36):
             per_turn, _ = e.step_flips(turns)
@@ -568,6 +569,7 @@ def test_narrow_board_takes_packed_slab(golhip, oracle, shape, code):
     and without (the tall 100000-row board only the shape choice)."""
     w, h = shape
     with golhip.Engine(w, h, k=16) as e:
+        e.set_board_kernel(False)  # 512^2 and 64^2 fit the whole-board kernel (tests/test_gpu_board.py)
         assert e.launch_kind(16) == ("slab", code)
         assert e.launch_kind(16, counts=True) == ("slab", code)
         if h > 20000:
