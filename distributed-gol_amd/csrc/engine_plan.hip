@@ -327,13 +327,13 @@ static int64_t max_band_rows(golhip_t h) {
 // Launch the K-generation stencil described by p (the register kernels or the level-split kernel
 // when the board asks for them).
 // Stable-slab skipping applies to a slab launch when: enabled, a production gol_slab2 shape, no flips,
-// the whole torus in one strip (bands wrap), and every band at least K rows tall (the 3 x 3 slabs
-// around a slab then cover the radius-K region its next K generations depend on).
+// the whole torus in one strip (bands wrap), and full bands at least K rows tall (the kernel checks
+// the slabs within K rows: the adjacent bands, and one more beyond the short last band).
 static bool activity_applies(golhip_t h, const RegKernel &rk, const StencilParams &q, int K) {
     if (!h->activity || h->split || q.diff || q.diff_stride > 0 || q.r1e > q.r1b || q.wrap_rows <= 0) return false;
     if (rk.kind != 3 || !stencil_slab_activity(K, rk.W, rk.S, rk.NC)) return false;
-    const int64_t rows = q.r0e - q.r0b, last = rows - (q.nbands - 1) * q.band;
-    return q.r0b == 0 && rows == q.wrap_rows && (q.nbands == 1 || last >= K);
+    const int64_t rows = q.r0e - q.r0b;
+    return q.r0b == 0 && rows == q.wrap_rows && q.band >= K && K <= 16;
 }
 
 // the slab launch's params (band = T rows, one slab per band and 62-word chunk)
@@ -524,8 +524,8 @@ int golhip_launch_plan(int64_t width, int64_t height, int strips, int k, int64_t
         *n = cnt;
         return cnt > cap && depths ? GOLHIP_ERR_CAP : GOLHIP_OK;
     }
-    LaunchPlanner plan(strip_cells, k, turns, strips == 1 && small_board(cells, Kfull), false, false,
-                       4096, stream);
+    LaunchPlanner plan(strip_cells, k, turns, strips == 1 && small_board(cells, Kfull), !stream, false,
+                       4096, stream);  // a register-slab board: its full depth (run_steps)
     while (plan.left > 0) {
         const int K = plan.next();
         if (depths && cnt < cap) depths[cnt] = K == 0 ? -(plan.last_M * plan.Kfull) : K;

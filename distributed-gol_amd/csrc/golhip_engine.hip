@@ -491,13 +491,15 @@ int run_steps(golhip_t h, int64_t turns, uint64_t *alive_per_turn, bool ring) {
     int bw = 0, br = 0;  // the whole-board kernel: W waves x R rows per segment
     const bool board = !ring && board_applies(h, &bw, &br);
     const int kmax = pick_k(h->k);
-    const bool stream = !ring && h->shards.size() == 1 &&
-                        pick_reg_kernel(h, h->shards[0].rows, kmax, counting).kind == 0 &&
-                        pick_split(h, h->shards[0].rows, kmax) <= 1;
+    const bool reg = !ring && !h->split && h->shards.size() == 1 &&
+                     pick_reg_kernel(h, h->shards[0].rows, kmax, counting).kind != 0;
+    const bool stream = !ring && h->shards.size() == 1 && !reg && pick_split(h, h->shards[0].rows, kmax) <= 1;
     // planned per strip (the band geometry and each GPU's launch time follow the strip), from the
-    // largest strip of the board, so every rank of a rank-mode board plans the same depths
+    // largest strip of the board, so every rank of a rank-mode board plans the same depths.  A
+    // register-slab board runs its tuned full depth (reg: fixed; best_rate_k's rates are the
+    // streaming kernel's), also without graphs, where only full-depth slabs skip stable slabs
     LaunchPlanner plan((double)h->L * (double)plan_rows(h), ring ? 1 : h->k, turns, !ring && graph_worthy(h, kmax),
-                       h->fixed_k || ring, h->track_flips, h->count_window, stream);
+                       h->fixed_k || ring || reg, h->track_flips, h->count_window, stream);
     if (counting) {
         // pinned host counts for calls that replay no graph (their graph replays would copy each
         // replay's counts into it); the others keep the device buffer and one copy returns them

@@ -606,8 +606,9 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
 // neighbourhood of slabs (bands and chunks wrap on the torus) did not change in the last generation
 // of the previous launch is constant for this launch's K generations: the Life update of a cell
 // depends on its radius-1 ball only, so a region of radius K around the slab that equals itself one
-// generation earlier keeps the slab fixed for K generations (each band is >= K rows tall and each
-// chunk >= 1 word wide -- the host checks -- so the 3 x 3 slabs cover that region).  Such a slab
+// generation earlier keeps the slab fixed for K generations (every band but the torus's last has
+// T >= K rows -- the host checks -- and the band beyond a short last band is checked too; a chunk is
+// >= 1 word wide, more than the K <= 16 bits the region reaches sideways).  Such a slab
 // copies its input to its output once (then both buffers agree: `same`), adds its cached alive
 // count to every generation's count slot and ends; the others compute as usual and record whether
 // their output changed in the last generation, and its alive count.  Bit-exact by construction;
@@ -637,9 +638,17 @@ __global__ __launch_bounds__(64 * W) void gol_slab2(const uint32_t *__restrict__
         uint32_t *const same = p.act + 2 * ngroups;
         uint32_t *const pop = p.act + 3 * ngroups;
         const int64_t bi = group / p.nchunks, ci = group % p.nchunks;
+        // the bands within K rows: the adjacent ones, and the next one beyond an adjacent band
+        // shorter than K rows (the short last band of the torus; every other band has T >= K rows)
+        auto short_band = [&](int64_t b) {
+            int y0, y1;
+            band_rows(p, (b + p.nbands) % p.nbands, y0, y1);
+            return y1 - y0 < K;
+        };
         uint32_t any = p.act_reset;
-        for (int db = -1; db <= 1; ++db) {
-            const int64_t bb = (bi + db + p.nbands) % p.nbands;
+        for (int db = -2; db <= 2; ++db) {
+            if ((db == -2 && !short_band(bi - 1)) || (db == 2 && !short_band(bi + 1))) continue;
+            const int64_t bb = ((bi + db) % p.nbands + p.nbands) % p.nbands;
             for (int dc = -1; dc <= 1; ++dc) any |= chg_in[bb * p.nchunks + (ci + dc + p.nchunks) % p.nchunks];
         }
         if (any == 0) {  // stable for K generations: output = input, every generation counts pop

@@ -278,3 +278,59 @@ def test_packed_slab_kernel(golhip, tuning, oracle, monkeypatch, code):
         got = [tuple(c) for c in e.flips().tolist()]
         assert np.array_equal(e.store(), exp)
     assert got == oracle.flips(before, exp)
+
+
+def _stamps(tuning, e):
+    """golhip_tuning_stamps_ex: (records, words per wave) of the last stamped launch."""
+    import ctypes
+
+    f = tuning.golhip_tuning_stamps_ex
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
+                  ctypes.POINTER(ctypes.c_int)]
+    f.restype = ctypes.c_int
+    n, wpw = ctypes.c_size_t(0), ctypes.c_int(0)
+    assert f(e._h, None, 0, ctypes.byref(n), ctypes.byref(wpw)) == 0
+    out = np.zeros(max(n.value, 8), dtype=np.uint64)
+    assert f(e._h, out.ctypes.data, out.size, ctypes.byref(n), ctypes.byref(wpw)) == 0
+    return out[: n.value].copy(), wpw.value
+
+
+def test_stamp_variant_k1_then_deep(golhip, tuning, monkeypatch):
+    """Pins the round-4 stamp-variant fix (csrc/tuning/engine_tuning.hip launch_params): only the
+    streaming gol_stencil takes the stamp buffer as its p.diff.  Round 4's K = 1 warm-up launch
+    (gol_step1) wrote its flips board over the 32 MiB stamp buffer (an illegal memory access,
+    profiles/r04/r04d_stamps_fault.log, r04f_stamps_fault.log).  Here, on the bench board (65536^2
+    random p = 0.5, seed 3) with GOLHIP_VARIANT=stamp: K = 1, then K = 12 launches, K = 1 again,
+    then K = 14 launches; the stamp records are the streaming kernel's (4 words per wave, start <=
+    end, shader cycles counted), a K = 1 launch leaves them untouched, and the board digest after
+    25 and 1008 turns matches tests/golden/synthetic_golden.json."""
+    import bench
+
+    monkeypatch.setenv("GOLHIP_VARIANT", "stamp")
+    n = 65536
+    d25, d1008 = bench.golden_digest(n, n, 3, 25), bench.golden_digest(n, n, 3, 1008)
+    assert d25 and d1008
+
+    def well_formed(st, wpw):
+        assert wpw == 4, wpw  # gol_stencil's record; gol_slab2's phase stamps are 8 words
+        rec = st.reshape(-1, 4)
+        assert len(rec) > 0
+        assert (rec[:, 0] > 0).all() and (rec[:, 1] >= rec[:, 0]).all() and (rec[:, 2] > 0).all()
+
+    with golhip.Engine(n, n, k=12, lib=tuning) as e:
+        assert e.launch_kind(12) == ("stream", 0)
+        e.set_fixed_k(True)
+        e.init_random(3)
+        e.step(1)  # gol_step1: no stamps
+        assert _stamps(tuning, e)[0].size == 0
+        e.step(24)  # 12 + 12
+        st, wpw = _stamps(tuning, e)
+        well_formed(st, wpw)
+        assert bench.board_digest(e.store_words(), 1) == d25
+        e.step(1)  # K = 1 again: the stamps of the last K = 12 launch stay as they were
+        st2, _ = _stamps(tuning, e)
+        assert np.array_equal(st, st2)
+        e.set_k(14)
+        e.step(982)  # 70 x 14 + a 2-deep tail
+        well_formed(*_stamps(tuning, e))
+        assert bench.board_digest(e.store_words(), 1) == d1008
