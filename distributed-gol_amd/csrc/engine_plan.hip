@@ -312,6 +312,7 @@ bool board_applies(golhip_t h, int *W, int *R) {
     // the production kernel family only, and no forced kernel or band (tests, tuning)
     if (!h->board_kernel || h->split || h->shards.size() != 1 || h->variant != kVariantProd) return false;
     if (h->force_split > 0 || h->force_tile >= 0 || h->force_slab >= 0 || h->band_rows > 0) return false;
+    if (h->board_kernel < 0 && h->height > kBoardAutoRows) return false;
     return stencil_board_shape(h->height, h->wd, W, R);
 }
 
@@ -332,6 +333,10 @@ static int64_t max_band_rows(golhip_t h) {
 static bool activity_applies(golhip_t h, const RegKernel &rk, const StencilParams &q, int K) {
     if (!h->activity || h->split || q.diff || q.diff_stride > 0 || q.r1e > q.r1b || q.wrap_rows <= 0) return false;
     if (rk.kind != 3 || !stencil_slab_activity(K, rk.W, rk.S, rk.NC)) return false;
+    // automatic: only boards with more slabs than CUs.  With one slab per CU a launch lasts as long
+    // as its slowest computed slab, so skipped slabs save nothing and the flags cost ~8 %
+    // (profiles/r05/r05l_act_probe.log)
+    if (h->activity < 0 && q.nbands * (int64_t)q.nchunks <= std::max(h->cus, 1)) return false;
     const int64_t rows = q.r0e - q.r0b;
     return q.r0b == 0 && rows == q.wrap_rows && q.band >= K && K <= 16;
 }
@@ -358,10 +363,11 @@ int ensure_activity(golhip_t h, Shard &s, int K, bool counting) {
     if (s.act) HIPCHK(h, hipFree(s.act));
     s.act = nullptr;
     s.act_cap = 0;
-    HIPCHK(h, hipMalloc(&s.act, sizeof(uint32_t) * 4 * (size_t)need));
+    HIPCHK(h, hipMalloc(&s.act, sizeof(uint32_t) * kActWords * (size_t)need));
+    HIPCHK(h, hipMemsetAsync(s.act, 0, sizeof(uint32_t) * kActWords * (size_t)need, s.compute));
     if (!s.act_stats) {
-        HIPCHK(h, hipMalloc(&s.act_stats, sizeof(unsigned long long) * 2));
-        HIPCHK(h, hipMemsetAsync(s.act_stats, 0, sizeof(unsigned long long) * 2, s.compute));
+        HIPCHK(h, hipMalloc(&s.act_stats, sizeof(unsigned long long) * 2 * kActStatSlots));
+        HIPCHK(h, hipMemsetAsync(s.act_stats, 0, sizeof(unsigned long long) * 2 * kActStatSlots, s.compute));
     }
     s.act_cap = need;
     h->act_valid = false;
@@ -373,7 +379,8 @@ hipError_t launch_auto(golhip_t h, int K, const uint32_t *in, uint32_t *out, con
     const int64_t rows_total = (p.r0e - p.r0b) + (p.r1e - p.r1b);
     if (const RegKernel rk = pick_reg_kernel(h, rows_total, K, slots != nullptr); rk.kind) {
         StencilParams q = slab_params(h, p, rk.out_rows());
-        const int64_t key[3] = {rk.out_rows(), q.nbands, q.nchunks};
+        // the flags' geometry: band rows, bands, chunks, and waves per slab (pop is per wave)
+        const int64_t key[3] = {rk.out_rows() * 64 + rk.W, q.nbands, q.nchunks};
         if (sh && sh->act && activity_applies(h, rk, q, K) && q.nbands * (int64_t)q.nchunks <= sh->act_cap) {
             q.act = sh->act;
             q.act_stats = sh->act_stats;
@@ -515,7 +522,7 @@ int golhip_launch_plan(int64_t width, int64_t height, int strips, int k, int64_t
                         !stencil_slab_supported(Kfull, 8, Kfull == 16 ? 12 : 8, Kfull == 16 ? 9 : 4) ||
                         waves1 > kSlabMaxWaves1PerCu * 256;
     size_t cnt = 0;
-    if (strips == 1 && stencil_board_shape(height, (int32_t)wd, nullptr, nullptr)) {
+    if (strips == 1 && height <= kBoardAutoRows && stencil_board_shape(height, (int32_t)wd, nullptr, nullptr)) {
         // the whole-board kernel: one launch per kBoardMaxK generations (of the count window)
         for (int64_t left = turns; left > 0; left -= kBoardMaxK) {
             if (depths && cnt < cap) depths[cnt] = (int32_t)std::min<int64_t>(left, kBoardMaxK);

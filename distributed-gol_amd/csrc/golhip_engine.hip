@@ -858,7 +858,8 @@ int golhip_edge_wait(golhip_t h, double *total_ms, int64_t *blocks) {
 
 int golhip_set_activity(golhip_t h, int enable) {
     if (!h) return GOLHIP_ERR_ARG;
-    h->activity = enable != 0;
+    if (enable < -1 || enable > 1) return GOLHIP_ERR_ARG;
+    h->activity = enable;
     h->act_valid = false;
     return GOLHIP_OK;
 }
@@ -870,10 +871,10 @@ int golhip_activity_stats(golhip_t h, int64_t *computed, int64_t *skipped) {
     unsigned long long v[2] = {0, 0};
     for (auto &s : h->shards)
         if (s.act_stats) {
-            unsigned long long t[2];
+            unsigned long long t[2 * kActStatSlots];
             HIPCHK(h, hipSetDevice(s.device));
             HIPCHK(h, hipMemcpy(t, s.act_stats, sizeof t, hipMemcpyDeviceToHost));
-            v[0] += t[0], v[1] += t[1];
+            for (int i = 0; i < 2 * kActStatSlots; ++i) v[i / kActStatSlots] += t[i];
         }
     if (computed) *computed = (int64_t)v[0];
     if (skipped) *skipped = (int64_t)v[1];
@@ -882,7 +883,8 @@ int golhip_activity_stats(golhip_t h, int64_t *computed, int64_t *skipped) {
 
 int golhip_set_board_kernel(golhip_t h, int enable) {
     if (!h) return GOLHIP_ERR_ARG;
-    h->board_kernel = enable != 0;
+    if (enable < -1 || enable > 1) return GOLHIP_ERR_ARG;
+    h->board_kernel = enable;
     return GOLHIP_OK;
 }
 

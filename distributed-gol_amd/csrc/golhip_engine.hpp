@@ -167,12 +167,14 @@ struct golhip_engine {
     // the boundary bands' waves raise their issue priority (StencilParams::prio)
     int edge_setprio = 1;
     int graph_mode = -1;  // golhip_set_graphs: -1 automatic, 0 never, 1 whenever the plan allows
-    // stable-slab skipping (golhip_set_activity; on by default): the slab flags on the shard hold
-    // the state of the last launch when act_valid, for slab geometry act_key (T, nbands, nchunks)
-    bool activity = true;
+    // stable-slab skipping (golhip_set_activity: -1 automatic -- boards with more slabs than CUs --,
+    // 0 off, 1 on): the slab flags on the shard hold the state of the last launch when act_valid,
+    // for slab geometry act_key (T * 64 + W, nbands, nchunks)
+    int activity = -1;
     bool act_valid = false;
-    // the whole-board kernel for the boards it fits (golhip_set_board_kernel; on by default)
-    bool board_kernel = true;
+    // the whole-board kernel (golhip_set_board_kernel: -1 automatic -- boards of at most
+    // kBoardAutoRows rows --, 0 off, 1 every board it fits)
+    int board_kernel = -1;
     int64_t act_key[3] = {0, 0, 0};
     // RCCL fail-fast (rank mode): every host wait on work that can depend on an RCCL transfer polls
     // ncclCommGetAsyncError against a deadline and fails the handle when it passes

@@ -28,6 +28,14 @@ namespace golhip {
 
 // Stencil launch: output rows [r0b, r0e) and [r1b, r1e) (second range may be empty) of the
 // strip after K generations, computed from the input strip.
+// StencilParams::act layout (uint32 offsets for G slabs): changed[par] at 4 G par (16 bytes per
+// slab), same at 8 G, pop at 9 G (16 per slab); kActWords * G in all.
+constexpr int kActWords = 25;
+__host__ __device__ inline int64_t act_chg_off(int par, int64_t G) { return 4 * G * par; }
+__host__ __device__ inline int64_t act_same_off(int64_t G) { return 8 * G; }
+__host__ __device__ inline int64_t act_pop_off(int64_t G) { return 9 * G; }
+constexpr int kActStatSlots = 64;  // StencilParams::act_stats: [computed x 64][skipped x 64]
+
 struct StencilParams {
     int64_t pitch;       // words between consecutive rows
     int64_t r0b, r0e;    // output range 0
@@ -55,13 +63,17 @@ struct StencilParams {
     // null in production; the tuning library's stamp handles: gol_slab2's per-wave phase stamps,
     // 8 uint64 per wave (golhip_tuning_stamps_ex, scripts/slab_stamps.py)
     uint64_t *stamp;
-    // Stable-slab skipping (gol_slab2 ACT, single-strip torus boards; null: off).  act holds four
-    // arrays of nbands * nchunks uint32, one entry per slab (workgroup): changed[0], changed[1] (did
-    // the slab's output change in the last generation of the launch that wrote it; this launch reads
-    // changed[act_par] and writes changed[act_par ^ 1]), same (both ping-pong buffers hold the slab's
-    // output region identically) and pop (its alive cells at that last generation).  act_reset: the
-    // flags are stale (a new board, another kernel ran): every slab computes and rewrites them.
-    // act_stats (nullable): two uint64 counters, slabs computed / slabs skipped.
+    // Stable-slab skipping (gol_slab2 ACT, single-strip torus boards; null: off).  act holds, per slab
+    // (workgroup) g of G = nbands * nchunks (offsets: act_*_off below, kActWords * G uint32 in all):
+    // changed[2] -- 16 bytes per slab, byte w: did wave w's output rows change in the last generation
+    // of the launch that wrote them (this launch reads changed[act_par], writes changed[act_par ^ 1]);
+    // same -- both ping-pong buffers hold the slab's output region identically; pop -- 16 uint32
+    // per slab, wave w's alive cells at that last generation.  Per-wave entries written with plain
+    // stores: one shared flag per slab took an OR / add atomic from every wave (+11 % kernel time on
+    // dense boards, profiles/r05/r05n_act_ablation.log).  act_reset: the flags are stale (a new
+    // board, another kernel or slab shape ran): every slab computes and rewrites them.
+    // act_stats (nullable): slabs computed / skipped, spread over kActStatSlots uint64 each (slot
+    // group % kActStatSlots: one shared counter serialised ~10 ns per workgroup at L2).
     uint32_t *act;
     unsigned long long *act_stats;
     int32_t act_par, act_reset;
@@ -219,6 +231,12 @@ hipError_t warm_stencil_tile(hipStream_t s);
 // and `height` = 4 W R rows in registers and runs K (runtime, <= kBoardMaxK) generations in one
 // launch.  stencil_board_shape: whether the board fits, and its (W waves, R rows per segment).
 constexpr int kBoardMaxK = 4096;
+// Automatic use (golhip_set_board_kernel -1): boards of at most this many rows.  One CU issues the
+// whole board's VALU work per generation, so the kernel gains while the board is short and loses
+// beyond: us per turn, board / slab kernels, calls of 1000 turns with counts
+// (profiles/r05/r05k_board_ab.log): 16^2 0.31 / 0.52, 64^2 0.37 / 0.53, 128^2 0.42 / 0.53,
+// 256^2 0.57 / 0.54, 512^2 0.88 / 0.55.
+constexpr int64_t kBoardAutoRows = 128;
 bool stencil_board_shape(int64_t height, int32_t wd, int *W, int *R);
 hipError_t launch_stencil_board(int K, int W, int R, const uint32_t *in_row0, uint32_t *out_row0,
                                 const StencilParams &p, unsigned long long *slots, hipStream_t s);

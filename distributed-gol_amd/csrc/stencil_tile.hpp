@@ -624,7 +624,6 @@ __global__ __launch_bounds__(64 * W) void gol_slab2(const uint32_t *__restrict__
     static_assert(!ACT || (LD == 0 && !ST), "stable-slab skipping: no flips, no stamps");
     __shared__ uint32_t ex[2][W + 2][4][64];  // as gol_slab: wave w's block is ex[par][w + 1]
     __shared__ uint32_t cnt_lds[COUNT ? K : 1][COUNT ? W : 1][64];
-    __shared__ uint32_t act_lds[2];  // ACT: the slab's changed bits (OR), its last-generation count
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     // XCD-aware order (gol_slab): XCD b % 8 gets a contiguous range of slabs
@@ -632,56 +631,6 @@ __global__ __launch_bounds__(64 * W) void gol_slab2(const uint32_t *__restrict__
     const int64_t per_xcd = (ngroups + kXcds - 1) / kXcds;
     const int64_t group = (int64_t)(blockIdx.x % kXcds) * per_xcd + blockIdx.x / kXcds;
     if (group >= ngroups) return;  // whole workgroup
-    if constexpr (ACT) {
-        uint32_t *const chg_in = p.act + (int64_t)p.act_par * ngroups;
-        uint32_t *const chg_out = p.act + (int64_t)(p.act_par ^ 1) * ngroups;
-        uint32_t *const same = p.act + 2 * ngroups;
-        uint32_t *const pop = p.act + 3 * ngroups;
-        const int64_t bi = group / p.nchunks, ci = group % p.nchunks;
-        // the bands within K rows: the adjacent ones, and the next one beyond an adjacent band
-        // shorter than K rows (the short last band of the torus; every other band has T >= K rows)
-        auto short_band = [&](int64_t b) {
-            int y0, y1;
-            band_rows(p, (b + p.nbands) % p.nbands, y0, y1);
-            return y1 - y0 < K;
-        };
-        uint32_t any = p.act_reset;
-        for (int db = -2; db <= 2; ++db) {
-            if ((db == -2 && !short_band(bi - 1)) || (db == 2 && !short_band(bi + 1))) continue;
-            const int64_t bb = ((bi + db) % p.nbands + p.nbands) % p.nbands;
-            for (int dc = -1; dc <= 1; ++dc) any |= chg_in[bb * p.nchunks + (ci + dc + p.nchunks) % p.nchunks];
-        }
-        if (any == 0) {  // stable for K generations: output = input, every generation counts pop
-            if (same[group] == 0) {  // the output buffer still holds an older generation: copy once
-                int ya, yb;
-                band_rows(p, bi, ya, yb);
-                const int colraw = (int)ci * kTileChunkWords + lane - 1;
-                const int col = (colraw + p.wd) % p.wd;
-                const int rowbytes = (int)(p.pitch * 4);
-                const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(
-                    out + (int64_t)ya * p.pitch, 0, (yb - ya) * rowbytes, kBufferRsrcWord3);
-                const LaneStore ls = lane_store<false>(lane, colraw, col, p.wd);
-                for (int r = w; r < yb - ya; r += W) {
-                    Words<1> v;
-                    v.w[0] = in[(int64_t)(ya + r) * p.pitch + col];
-                    golhip::store_row<1, false>(orsrc, ls, v, r * rowbytes);
-                }
-            }
-            if constexpr (COUNT)
-                if (w == 0 && lane < K && pop[group])
-                    __hip_atomic_fetch_add(&slots[lane * kCountSlots + (int)(group & (kCountSlots - 1))],
-                                           (unsigned long long)pop[group], __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-            if (w == 0 && lane == 0) {  // vector stores (lane 0), never the scalar path
-                chg_out[group] = 0u;
-                same[group] = 1u;
-                if (p.act_stats)
-                    __hip_atomic_fetch_add(&p.act_stats[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            return;
-        }
-        if (w == 0 && lane == 0) act_lds[0] = act_lds[1] = 0u;  // ordered by the first barrier
-    }
     uint32_t act_chg = 0, act_pop = 0;  // ACT: this lane's changed bits / count at the last generation
     if constexpr (YP)
         if (w >= W / 2) __builtin_amdgcn_s_setprio(1);
@@ -698,6 +647,29 @@ __global__ __launch_bounds__(64 * W) void gol_slab2(const uint32_t *__restrict__
     const int colraw = (int)chunk * kTileChunkWords + lane - 1;
     const int col = (colraw + p.wd) % p.wd;
     const int rowbytes = (int)(p.pitch * 4);
+    // ACT: the changed bytes of the slabs within K rows, loaded before the rows (one round trip,
+    // no branch or division in between): the adjacent bands, and the next one beyond an adjacent
+    // band shorter than K rows (the short last band of the torus; every other band has T >= K
+    // rows), x the adjacent chunks; 16 bytes (one per wave) per slab, lanes 0..59 one dword each
+    uint32_t act_f = 0;
+    if constexpr (ACT) {
+        const int nb = (int)p.nbands, nc = (int)p.nchunks;
+        const int bi = (int)bandi, ci = (int)chunk;
+        const bool short_last = (int)(p.r0e - (int64_t)(nb - 1) * p.band) < K;  // slab_params: uniform bands
+        auto wrap = [](int v, int n) {  // |v| < 3 n
+            v = v < 0 ? v + n : v;
+            v = v < 0 ? v + n : v;
+            v = v >= n ? v - n : v;
+            return v >= n ? v - n : v;
+        };
+        const int bm1 = wrap(bi - 1, nb), bp1 = wrap(bi + 1, nb);
+        const int l = lane < 60 ? lane : 0;  // every lane loads (lanes 60..63 masked below)
+        const int i = l / 12, j = (l >> 2) % 3, d = l & 3;
+        const int bb = i == 0 ? (short_last && bm1 == nb - 1 ? wrap(bi - 2, nb) : bi)
+                     : i == 1 ? bm1 : i == 2 ? bi : i == 3 ? bp1
+                                               : (short_last && bp1 == nb - 1 ? wrap(bi + 2, nb) : bi);
+        act_f = p.act[act_chg_off(p.act_par, ngroups) + (int64_t)(bb * nc + wrap(ci + j - 1, nc)) * 4 + d];
+    }
     uint32_t c[S + 2];  // rows 1..S of this wave (c[0], c[S + 1] unused)
     c[0] = c[S + 1] = 0;
     load_rows<1, S>(c, in, p, ya - K + w * S, col);
@@ -715,6 +687,50 @@ __global__ __launch_bounds__(64 * W) void gol_slab2(const uint32_t *__restrict__
     const LaneStore ls = lane_store<false>(lane, colraw, col, p.wd);
     const bool count_lane = lane >= 2 && colraw <= p.wd;
     const int o0 = w * S - K;  // output row of c[1]
+    if constexpr (ACT) {
+        uint32_t *const same = p.act + act_same_off(ngroups);
+        const uint32_t *const pop = p.act + act_pop_off(ngroups) + group * 16;  // one count per wave
+        // first use of the flags after the row loads are issued (the wait is vmcnt(S), not 0)
+        const int nbytes = W - 4 * (lane & 3);  // this dword's bytes that belong to waves of this shape
+        const uint32_t mask = lane >= 60 || nbytes <= 0 ? 0u : nbytes >= 4 ? ~0u : (1u << (8 * nbytes)) - 1u;
+        if (!p.act_reset && __builtin_amdgcn_ballot_w64((act_f & mask) != 0u) == 0) {
+            // stable for K generations: output = input, every generation counts the slab's alive cells
+            if (same[group] == 0) {  // the output buffer still holds an older generation: store the
+                                     // rows just loaded (this wave's rows of the band) once
+#pragma unroll
+                for (int r = 1; r <= S; ++r) {
+                    const int o = o0 + r - 1;
+                    Words<1> v;
+                    v.w[0] = c[r];
+                    golhip::store_row<1, false>(orsrc, ls, v, o >= 0 && o < nrows ? o * rowbytes : kOutOfRange);
+                }
+            }
+            if (w == 0) {  // vector stores / atomics from lanes, never the scalar path
+                if constexpr (COUNT) {
+                    const uint32_t n = __builtin_amdgcn_readlane(wave_sum_dpp(lane < W ? pop[lane] : 0u), 63);
+                    if (lane < K && n)
+                        __hip_atomic_fetch_add(&slots[lane * kCountSlots + (int)(group & (kCountSlots - 1))],
+                                               (unsigned long long)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                if (lane < 4) p.act[act_chg_off(p.act_par ^ 1, ngroups) + group * 4 + lane] = 0u;
+                if (lane == 0) {
+                    same[group] = 1u;
+                    if (p.act_stats)
+                        __hip_atomic_fetch_add(&p.act_stats[kActStatSlots + (int)(group & (kActStatSlots - 1))], 1ull,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            return;
+        }
+        // computed: the two buffers now differ on this slab; every wave writes its changed byte and
+        // count at its end (plain stores: no clearing, no atomics on the flags)
+        if (w == 0 && lane == 0) {
+            same[group] = 0u;
+            if (p.act_stats)
+                __hip_atomic_fetch_add(&p.act_stats[(int)(group & (kActStatSlots - 1))], 1ull, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
     if constexpr (COUNT)
         for (int j = 0; j < K; ++j) cnt_lds[j][w][lane] = 0;
     if (w == 0)
@@ -890,20 +906,12 @@ __global__ __launch_bounds__(64 * W) void gol_slab2(const uint32_t *__restrict__
                 r[6] = (uint64_t)group, r[7] = (uint64_t)w;
             }
         }
-    if constexpr (ACT) {  // the slab's flags for the next launch
+    if constexpr (ACT) {  // this wave's share of the slab's flags for the next launch
         const bool chg = __builtin_amdgcn_ballot_w64(act_chg != 0u) != 0;
         const uint32_t cnt = wave_sum_dpp(act_pop);
         if (lane == 63) {
-            if (cnt) __hip_atomic_fetch_add(&act_lds[1], cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (chg) __hip_atomic_fetch_or(&act_lds[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        __syncthreads();
-        if (w == 0 && lane == 0) {
-            p.act[(int64_t)(p.act_par ^ 1) * ngroups + group] = act_lds[0];
-            p.act[2 * ngroups + group] = 0u;  // the two buffers now differ on this slab
-            p.act[3 * ngroups + group] = act_lds[1];
-            if (p.act_stats)
-                __hip_atomic_fetch_add(&p.act_stats[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            reinterpret_cast<uint8_t *>(p.act + act_chg_off(p.act_par ^ 1, ngroups) + group * 4)[w] = chg ? 1 : 0;
+            p.act[act_pop_off(ngroups) + group * 16 + w] = cnt;
         }
     }
 }

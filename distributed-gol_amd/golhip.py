@@ -617,12 +617,15 @@ class Engine:
     def timing(self, enable: bool):
         self._check(self._L.golhip_timing(self._h, int(enable)))
 
-    def set_activity(self, enable: bool):
-        """Stable-slab skipping of the small-board slab launches (golhip_set_activity; default on)."""
+    def set_activity(self, enable: int):
+        """Stable-slab skipping of the slab launches (golhip_set_activity): -1 automatic (the
+        default: boards with more slabs than CUs), 0 / False off, 1 / True on."""
         self._check(self._L.golhip_set_activity(self._h, int(enable)))
 
-    def set_board_kernel(self, enable: bool):
-        """The whole-board kernel for boards that fit one workgroup (golhip_set_board_kernel)."""
+    def set_board_kernel(self, enable: int):
+        """The whole-board kernel for boards that fit one workgroup (golhip_set_board_kernel): -1
+        automatic (the default: boards of at most 128 rows), 0 / False off, 1 / True every board
+        it fits."""
         self._check(self._L.golhip_set_board_kernel(self._h, int(enable)))
 
     def activity_stats(self) -> tuple[int, int]:

@@ -255,19 +255,23 @@ int golhip_set_comm_timeout(golhip_t h, int64_t ms);
  * GOLHIP_ERR_STATE if the communicator has not failed. */
 int golhip_comm_abort(golhip_t h);
 int golhip_sync(golhip_t h);                         /* wait for all queued device work */
-/* The whole-board kernel (default on): a single-strip board of 128, 256 or 512 torus cells per row
- * (any width up to 512 whose lcm with 128 is one of them: the reference's 16/64/128/256/512 sizes)
- * and 4 W R rows (4 ... 512) runs in ONE workgroup holding the whole torus in registers, every
- * golhip_step call as one launch per 4096 generations: no temporal-blocking trapezoid, no halo
- * lanes, no launch boundary inside a call.  enable = 0 keeps the multi-workgroup slab kernels
- * (A/B).  golhip_launch_kind reports it as kind 4 (*param = 100 * waves + rows per segment). */
+/* The whole-board kernel: a single-strip board of 128, 256 or 512 torus cells per row (any width up
+ * to 512 whose lcm with 128 is one of them: the reference's 16/64/128/256/512 sizes) and 4 W R rows
+ * (4 ... 512) runs in ONE workgroup holding the whole torus in registers, every golhip_step call as
+ * one launch per 4096 generations: no temporal-blocking trapezoid, no halo lanes, no launch
+ * boundary inside a call.  enable = -1 (default): boards of at most 128 rows (one CU does the
+ * board's whole VALU work per generation: faster than the multi-workgroup slabs up to 128 rows,
+ * slower from 256), 1: every board it fits, 0: never (A/B).  golhip_launch_kind reports it as
+ * kind 4 (*param = 100 * waves + rows per segment).  GOLHIP_ERR_ARG outside -1 .. 1. */
 int golhip_set_board_kernel(golhip_t h, int enable);
-/* Stable-slab skipping (default on): the register-slab launches of single-strip small boards skip
- * every slab whose neighbourhood did not change in the previous launch's last generation -- Life's
- * radius-1 rule keeps such a slab fixed for the launch's K generations -- copying it once and
- * counting its cached alive cells for each generation.  Results are identical either way (a settled
- * board, e.g. configs[4] after ~70 000 turns, skips nearly every slab).  enable = 0 computes every
- * slab (A/B, dense-equivalent timing). */
+/* Stable-slab skipping: the register-slab launches of single-strip boards skip every slab whose
+ * neighbourhood did not change in the previous launch's last generation -- Life's radius-1 rule
+ * keeps such a slab fixed for the launch's K generations -- copying it once and counting its cached
+ * alive cells for each generation.  Results are identical either way.  enable = -1 (default):
+ * boards with more slabs than CUs (with one slab per CU a launch lasts as long as its slowest
+ * computed slab, so skipping saves nothing there; sparse 16384^2 runs 1.7x faster, dense boards
+ * pay ~8 % for the flags), 1: every eligible launch, 0: never (A/B).  GOLHIP_ERR_ARG outside
+ * -1 .. 1. */
 int golhip_set_activity(golhip_t h, int enable);
 /* Slab launches computed / skipped on this handle since it was created (stable-slab skipping). */
 int golhip_activity_stats(golhip_t h, int64_t *computed, int64_t *skipped);

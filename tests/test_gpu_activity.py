@@ -110,6 +110,7 @@ def test_new_board_and_other_kernels_reset_the_flags(golhip, oracle):
     sparse = sparse_board(h, w, seed=9)
     dense = oracle.unpack(oracle.init_random(w, h, seed=21), w)
     with golhip.Engine(w, h, k=16) as e:
+        e.set_activity(1)  # forced: 80 slabs, automatic skipping needs more slabs than CUs
         e.load(sparse)
         e.step(800, counts=True)
         assert e.activity_stats()[1] > 0
@@ -137,6 +138,7 @@ def test_configs4_prefix_matches_golden_counts(golhip):
     golhip.place(b, golhip.parse_rle((GOLDEN / "r_pentomino.rle").read_text()), 2048, 2048)
     exp = (int((b == 255).sum()) + np.cumsum(deltas[:20000].astype(np.int64)))
     with golhip.Engine(4096, 4096, k=16) as e:
+        e.set_activity(1)  # forced: 237 slabs, automatic skipping needs more slabs than CUs
         e.load(b)
         c = e.step(20000, counts=True)
         computed, skipped = e.activity_stats()
@@ -149,3 +151,24 @@ def test_configs4_prefix_matches_golden_counts(golhip):
         e.load(b)
         c_off = e.step(4096, counts=True)
     assert np.array_equal(c_off.astype(np.int64), exp[:4096])
+
+
+def test_automatic_policy_by_slab_count(golhip, oracle):
+    """Automatic skipping (the default, golhip_set_activity(-1)) runs only on boards with more slabs
+    than CUs: at one slab per CU a launch lasts as long as its slowest computed slab, so skipping
+    saves nothing there and its flags cost time (profiles/r05/r05l_act_probe.log).  4096^2 (237
+    slabs): never skips; 8192^2 sparse (384 slabs): skips, every count against the oracle."""
+    b = sparse_board(4096, 4096, seed=3)
+    with golhip.Engine(4096, 4096, k=16) as e:
+        e.load(b)
+        e.step(256, counts=True)
+        assert e.activity_stats() == (0, 0)
+    b = sparse_board(8192, 8192, seed=4, n_gliders=10)
+    with golhip.Engine(8192, 8192, k=16) as e:
+        e.load(b)
+        c = e.step(320, counts=True)
+        computed, skipped = e.activity_stats()
+        got = e.store()
+    ref, ref_c = oracle.packed_run(b, 320)
+    assert np.array_equal(c.astype(np.int64), ref_c) and np.array_equal(got, ref)
+    assert skipped > computed > 0, (computed, skipped)

@@ -1,6 +1,6 @@
 """The whole-board kernel (stencil_board.hip, gol_board): boards of 128 / 256 / 512 torus cells per
 row and 4 W R rows run in ONE workgroup for a whole golhip_step call (one launch per 4096
-generations).  Bit-exact against the oracle -- every count of every turn, the board, the last
+generations); automatic up to 128 rows, forced here (golhip_set_board_kernel(1)) on taller ones.  Bit-exact against the oracle -- every count of every turn, the board, the last
 generation's flips -- on every (W, R) shape, widths whose torus is replicated (16, 64 cells), calls
 of 1 turn (the flips of a one-generation step), of many generations in one launch, across count
 windows, and against the same engine with the kernel off (the multi-workgroup slabs).
@@ -20,6 +20,9 @@ pytestmark = pytest.mark.gpu
 def test_board_kernel_matches_oracle(golhip, oracle, w, h):
     board = (np.random.default_rng(w * 7 + h).random((h, w)) < 0.37).astype(np.uint8) * 255
     with golhip.Engine(w, h, k=16) as e:
+        # automatic up to 128 rows (kBoardAutoRows); forced here for every shape
+        assert (e.launch_kind(16)[0] == "board") == (h <= 128), e.launch_kind(16)
+        e.set_board_kernel(1)
         assert e.launch_kind(16)[0] == "board", e.launch_kind(16)
         e.load(board)
         c1 = e.step(1, counts=True)
@@ -67,12 +70,14 @@ def test_board_kernel_long_calls_across_count_windows(golhip, oracle):
     _, _, board = oracle.read_pgm(REF / "images/512x512.pgm")
     csv = oracle.read_alive_csv(REF / "check/alive/512x512.csv")
     with golhip.Engine(512, 512, k=16) as e:
+        e.set_board_kernel(1)  # forced (automatic only up to 128 rows)
         e.load(board)
         c = e.step(10000, counts=True)
         assert [int(x) for x in c] == [csv[t] for t in range(1, 10001)]
         tail = e.step(9, counts=True)
         assert [int(x) for x in tail] == [5565 if t % 2 == 0 else 5567 for t in range(10001, 10010)]
     with golhip.Engine(512, 512, k=16) as e:
+        e.set_board_kernel(1)
         e.set_count_window(128)
         e.load(board)
         c = e.step(1000, counts=True)
@@ -96,6 +101,7 @@ def test_board_kernel_on_and_off_identical(golhip, oracle):
 
 
 def test_board_launch_plan(golhip):
-    assert golhip.launch_plan(512, 512, 16, 100) == [100]
-    assert golhip.launch_plan(512, 512, 16, 10000) == [4096, 4096, 1808]
+    assert golhip.launch_plan(128, 128, 16, 100) == [100]
+    assert golhip.launch_plan(64, 64, 16, 10000) == [4096, 4096, 1808]
+    assert golhip.launch_plan(512, 512, 16, 100) != [100]  # 512 rows: the slab kernels (automatic)
     assert golhip.launch_plan(512, 512, 16, 100, strips=2) != [100]  # strips: not the board kernel

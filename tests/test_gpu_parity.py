@@ -170,8 +170,9 @@ def test_step_flips_sdl_512_every_count(golhip, oracle):
     shadow = (board == 255)
     with golhip.Engine(512, 512, k=16) as e:
         e.load(board)
-        # golhip_step runs this board with the whole-board kernel; the flips ring with slabs
-        assert e.launch_kind(16)[0] == "board"
+        # 512 rows: golhip_step runs this board with the slab kernels (the whole-board kernel is
+        # automatic up to 128 rows); the flips ring with slabs
+        assert e.launch_kind(16)[0] == "slab"
         t0 = 0
         for turns in (64, 36):
             per_turn, _ = e.step_flips(turns)
