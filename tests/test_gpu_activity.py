@@ -172,3 +172,20 @@ def test_automatic_policy_by_slab_count(golhip, oracle):
     ref, ref_c = oracle.packed_run(b, 320)
     assert np.array_equal(c.astype(np.int64), ref_c) and np.array_equal(got, ref)
     assert skipped > computed > 0, (computed, skipped)
+
+
+def test_policy_switches_take_minus_one_zero_one(golhip):
+    """golhip_set_activity / golhip_set_board_kernel: -1 automatic, 0 off, 1 on; anything else is
+    GOLHIP_ERR_ARG and leaves the setting alone."""
+    with golhip.Engine(64, 64, k=16) as e:
+        assert e.launch_kind(16)[0] == "board"  # automatic: 64 rows
+        for bad in (2, -2, 7):
+            with pytest.raises(golhip.GolHipError):
+                e.set_board_kernel(bad)
+            with pytest.raises(golhip.GolHipError):
+                e.set_activity(bad)
+        assert e.launch_kind(16)[0] == "board"
+        e.set_board_kernel(0)
+        assert e.launch_kind(16)[0] == "slab"
+        e.set_board_kernel(-1)
+        assert e.launch_kind(16)[0] == "board"
