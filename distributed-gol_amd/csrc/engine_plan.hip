@@ -208,7 +208,7 @@ int pick_split(golhip_t h, int64_t rows_total, int K) {
 // LDS).  They replace the streaming band's pipeline fill (2K rows per band, one dependency chain
 // per wave) by a K-row trapezoid per tile/slab with every row of a generation independent; they
 // win where the streaming kernel cannot get both tall bands and enough waves (small boards;
-// profiles/r02/tune_tile.txt).
+// profiles/r02/small_boards.txt).
 RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K, bool counting) {
     RegKernel rk;
     if (!variant_is_production_family(h->variant) || h->split) return rk;

@@ -52,7 +52,7 @@ constexpr int64_t kStampWaves = 1 << 20;  // tuning library: waves of the per-wa
 constexpr int64_t kStageBytes = 64ll << 20;
 constexpr int kGraphGens = 128;  // generations per graph replay (<= count_window)
 // Long runs replay larger graphs: each replay of a counting graph ends in a count finalize and a
-// copy of its counts (~17 us together on a 5120^2 board, profiles/r02/small_board_timeline.txt),
+// copy of its counts (~17 us together on a 5120^2 board, profiles/r02/small_board_timeline_split_k16.txt),
 // paid per 4096 generations instead of per 128 (bounded by the count window).
 constexpr int kGraphGensBig = 4096;
 constexpr double kLaunchOverheadUs = 4.0;

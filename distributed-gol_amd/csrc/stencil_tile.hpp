@@ -6,7 +6,7 @@
 // Each wave is one long dependency chain (row after row, level after level) whose pipeline fill
 // costs 2K rows, so it needs tall bands and many waves.  A small board cannot give it both.  At
 // 5120^2 a K = 16 launch ran 23.7 us, about 12x the VALU time of its useful work
-// (profiles/r02/small_board_timeline.txt): short bands, about one wave per SIMD, and every step
+// (profiles/r02/small_board_timeline_split_k16.txt): short bands, about one wave per SIMD, and every step
 // waiting on the previous level.
 //
 // gol_tile turns the loop around.  A wave loads a whole tile into VGPRs: R = T + 2K rows of its
