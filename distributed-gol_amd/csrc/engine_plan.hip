@@ -73,6 +73,15 @@ int best_rate_k(int kmax, double cells) {
     return best;
 }
 
+// Register-slab boards: a slab launch is latency-bound (a chain of barrier-bound generations plus a
+// ~3 us launch boundary, about the same at any depth), so the tail takes the fewest launches: the
+// largest depth of the slab kernels' {16, 12, 8, 4, 2, 1} that fits.
+int slab_first_k(int64_t n, int kmax) {
+    for (int K : {16, 12, 8, 4, 2})
+        if (K <= n && K <= kmax && stencil_k_supported(K)) return K;
+    return 1;
+}
+
 // Launch depths for `n` remaining generations (n < 2 * kmax): the sequence of supported depths
 // <= kmax summing to n with the least modelled time sum(cells * K / rate(K) + overhead).  The
 // greedy largest-first split ran 20 turns as 16 + 4 (the 4-level launch at half the rate);
@@ -263,7 +272,7 @@ RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K, bool counting) 
     // (1600 turns, every count: 512^2 4 x 3 0.570 us/turn vs 0.811 for gol_slab2 12 x 7; 4096 x 512
     // 6 x 3 0.598 (4 x 3 with 1024 workgroups 0.806); 640^2 (P = 2) 6 x 3 0.604 / 8 x 3 0.590 vs
     // 0.809; without counts 0.37 - 0.42 vs 0.70: profiles/r04/r04p4_narrow_sweep.log, r04p5)
-    if (K == 16 && h->wd <= 30) {
+    if ((K == 16 || K == 12 || K == 8 || K == 4 || K == 2) && h->wd <= 30) {  // round 5: also the tail depths
         const int P = (int)(64 / (h->wd + 2));
         for (const int W : {4, 6, 8}) {
             const int T = W * P * 3 - 2 * K;
@@ -450,11 +459,12 @@ bool small_board(double cells, int K) { return cells * K <= 8e9; }
 // replays use the best-rate depth too (16384^2: 64.5 vs 55.3 TCUPS at K = 12 vs 16,
 // profiles/r02/r02ae_depth_by_size.txt); the register kernels are tuned at the full depth.
 LaunchPlanner::LaunchPlanner(double cells_, int k, int64_t turns, bool small, bool fixed, bool keep_last_,
-                             int window, bool stream)
+                             int window, bool stream, bool reg_)
     : cells(cells_),
       Kfull(small && stream && !fixed ? best_rate_k(pick_k(k), cells_) : pick_k(k)),
       left(turns),
       keep_last(keep_last_) {
+    reg = reg_;
     M = std::max(2, (kGraphGens / Kfull) & ~1);
     Mbig = std::max(M, (std::min(kGraphGensBig, window) / Kfull) & ~1);
     graphs = small && turns >= (int64_t)M * Kfull + (keep_last ? 1 : 0);
@@ -468,7 +478,7 @@ int LaunchPlanner::next() {
             last_M = m;
             return 0;
         }
-    const int K = left >= 2 * (int64_t)Kbulk ? Kbulk : plan_first_k(left, Kfull, cells);
+    const int K = left >= 2 * (int64_t)Kbulk ? Kbulk : reg ? slab_first_k(left, Kfull) : plan_first_k(left, Kfull, cells);
     left -= K;
     return K;
 }
@@ -532,7 +542,7 @@ int golhip_launch_plan(int64_t width, int64_t height, int strips, int k, int64_t
         return cnt > cap && depths ? GOLHIP_ERR_CAP : GOLHIP_OK;
     }
     LaunchPlanner plan(strip_cells, k, turns, strips == 1 && small_board(cells, Kfull), !stream, false,
-                       4096, stream);  // a register-slab board: its full depth (run_steps)
+                       4096, stream, !stream);  // a register-slab board: full depth, fewest launches (run_steps)
     while (plan.left > 0) {
         const int K = plan.next();
         if (depths && cnt < cap) depths[cnt] = K == 0 ? -(plan.last_M * plan.Kfull) : K;

@@ -499,7 +499,7 @@ int run_steps(golhip_t h, int64_t turns, uint64_t *alive_per_turn, bool ring) {
     // register-slab board runs its tuned full depth (reg: fixed; best_rate_k's rates are the
     // streaming kernel's), also without graphs, where only full-depth slabs skip stable slabs
     LaunchPlanner plan((double)h->L * (double)plan_rows(h), ring ? 1 : h->k, turns, !ring && graph_worthy(h, kmax),
-                       h->fixed_k || ring || reg, h->track_flips, h->count_window, stream);
+                       h->fixed_k || ring || reg, h->track_flips, h->count_window, stream, reg && !h->fixed_k);
     if (counting) {
         // pinned host counts for calls that replay no graph (their graph replays would copy each
         // replay's counts into it); the others keep the device buffer and one copy returns them
@@ -859,6 +859,13 @@ int golhip_edge_wait(golhip_t h, double *total_ms, int64_t *blocks) {
 int golhip_set_activity(golhip_t h, int enable) {
     if (!h) return GOLHIP_ERR_ARG;
     if (enable < -1 || enable > 1) return GOLHIP_ERR_ARG;
+    if (enable != h->activity && !h->graphs.empty()) {
+        // captured replays bake the slab kernel (with or without skipping) in: recapture
+        int rc = sync_all(h);
+        if (rc) return rc;
+        for (auto &g : h->graphs) (void)hipGraphExecDestroy(g.exec);
+        h->graphs.clear();
+    }
     h->activity = enable;
     h->act_valid = false;
     return GOLHIP_OK;

@@ -314,6 +314,7 @@ int pick_k(int n);
 double launch_rate_tcups(int K, double cells = 0.0);
 int best_rate_k(int kmax, double cells);
 int plan_first_k(int64_t n, int kmax, double cells);
+int slab_first_k(int64_t n, int kmax);
 int64_t auto_band(golhip_t h, int64_t rows_total, int K, int64_t reserve_waves = 0, bool counting = false);
 int pick_split(golhip_t h, int64_t rows_total, int K);
 struct RegKernel {
@@ -344,8 +345,9 @@ struct LaunchPlanner {
     bool graphs;
     int64_t left;
     bool keep_last;  // the last generation is always a plain launch (it writes the flips)
+    bool reg = false;  // register-slab board: tails by fewest launches (slab_first_k)
     LaunchPlanner(double cells_, int k, int64_t turns, bool small, bool fixed = false,
-                  bool keep_last_ = false, int window = 4096, bool stream = false);
+                  bool keep_last_ = false, int window = 4096, bool stream = false, bool reg_ = false);
     int next();
     // true when this plan replays at least one graph (the call's counts then come from per-replay
     // copies, which pinned host memory makes slower: run_steps)

@@ -14,9 +14,14 @@ namespace golhip {
 // at 5120^2 with 16 x 6, 0.730 at 4096^2 with 12 x 7; profiles/r04/r04u_tune.log).  Narrow boards
 // (wd <= 30) run the packed gol_slabp (NC = 14) at 4 / 6 / 8 waves x 3 rows (512^2 with every
 // count 0.811 -> 0.570 us/turn, without 0.708 -> 0.373: profiles/r04/r04p4_narrow_sweep.log).
+// Round 5: the packed slab at depths 2 / 4 / 8 / 12 too, for the tails of narrow-board calls
+// (configs[0]'s 100 turns ended in gol_slab 12 + 8 launches at 11.8 + 8.0 us against ~7 us per
+// packed launch: profiles/r05/r05p_cfg0_timeline.log).
 #define GOLHIP_SLAB_PROD_CONFIGS(X) \
     X(8, 8, 8, 4) X(12, 8, 8, 4) X(16, 8, 12, 9) X(16, 16, 6, 9) X(16, 12, 8, 9) X(16, 12, 7, 9) \
-    X(16, 16, 6, 12) X(16, 12, 7, 12) X(16, 12, 8, 12) X(16, 4, 3, 14) X(16, 6, 3, 14) X(16, 8, 3, 14)
+    X(16, 16, 6, 12) X(16, 12, 7, 12) X(16, 12, 8, 12) X(16, 4, 3, 14) X(16, 6, 3, 14) X(16, 8, 3, 14) \
+    X(12, 4, 3, 14) X(12, 6, 3, 14) X(12, 8, 3, 14) X(8, 4, 3, 14) X(8, 6, 3, 14) X(8, 8, 3, 14) \
+    X(4, 4, 3, 14) X(4, 6, 3, 14) X(4, 8, 3, 14) X(2, 4, 3, 14) X(2, 6, 3, 14) X(2, 8, 3, 14)
 
 static bool slab_prod_supported(int K, int W, int S, int NC) {
 #define GOLHIP_X(KK, WW, SS, NN) \

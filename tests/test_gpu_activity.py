@@ -189,3 +189,26 @@ def test_policy_switches_take_minus_one_zero_one(golhip):
         assert e.launch_kind(16)[0] == "slab"
         e.set_board_kernel(-1)
         assert e.launch_kind(16)[0] == "board"
+
+
+def test_switching_skipping_recaptures_graphs(golhip, oracle):
+    """Replays captured with skipping on must not keep running it after set_activity(0) (and the
+    reverse): the switch drops the captured graphs.  Stats count only the skipping launches."""
+    b = sparse_board(8192, 8192, seed=11, n_gliders=8)
+    with golhip.Engine(8192, 8192, k=16) as e:
+        e.set_graphs(1)
+        e.set_activity(1)
+        e.load(b)
+        c1 = e.step(256, counts=True)  # graph replays with skipping
+        s1 = e.activity_stats()
+        assert s1[1] > 0
+        e.set_activity(0)
+        c2 = e.step(256, counts=True)  # recaptured without skipping
+        assert e.activity_stats() == s1
+        e.set_activity(1)
+        c3 = e.step(256, counts=True)
+        assert e.activity_stats()[0] > s1[0]
+        got = e.store()
+    ref, ref_c = oracle.packed_run(b, 768)
+    assert np.array_equal(np.concatenate([c1, c2, c3]).astype(np.int64), ref_c)
+    assert np.array_equal(got, ref)

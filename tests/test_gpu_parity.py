@@ -593,11 +593,15 @@ def test_counts_pinned_and_device_buffers_interleaved(golhip, oracle):
     """Calls of at most 127 turns return their per-turn counts through pinned host memory, longer
     calls through the device buffer (graph replays): interleaved on one engine, every count and
     the board against the oracle."""
-    words = oracle.init_random(512, 512, seed=31)
-    ref = words.copy()
-    with golhip.Engine(512, 512, k=16) as e:
-        e.load_words(words)
-        for turns in (100, 5000, 37, 127, 128, 4096, 1):
-            counts = e.step(turns, counts=True)
-            assert np.array_equal(counts.astype(np.int64), oracle.packed_run_words(ref, turns)), turns
-        assert np.array_equal(e.store_words(), ref)
+    for k, calls in ((16, (100, 5000, 37, 127, 128, 4096, 1)),
+                     # K = 12: a replayed graph is 10 x 12 = 120 generations, so calls of 120-127
+                     # turns replay one (device buffer) although they are under 128 (ADVICE r04)
+                     (12, (119, 120, 121, 127, 5, 240))):
+        words = oracle.init_random(512, 512, seed=31 + k)
+        ref = words.copy()
+        with golhip.Engine(512, 512, k=k) as e:
+            e.load_words(words)
+            for turns in calls:
+                counts = e.step(turns, counts=True)
+                assert np.array_equal(counts.astype(np.int64), oracle.packed_run_words(ref, turns)), (k, turns)
+            assert np.array_equal(e.store_words(), ref)
