@@ -560,7 +560,7 @@ def configs_leg() -> dict:
     res["cfg1_512x100"] = {"us_per_turn": round(dt / 100 * 1e6, 3), "median_of": 5, "kernel": kind,
                            "bit_exact_vs_reference_fixture": bool(ok and ok_b),
                            # A/B: the single-workgroup whole-board kernel forced (automatic only up to
-                           # 128 rows: one CU's VALU work per generation grows with the board)
+                           # 256 rows: one CU's VALU work per generation grows with the board)
                            "whole_board_kernel_forced": {"kernel": kind_b,
                                                          "us_per_turn": round(dt_b / 100 * 1e6, 3)}}
     # configs[1]

@@ -236,7 +236,7 @@ constexpr int kBoardMaxK = 4096;
 // beyond: us per turn, board / slab kernels, calls of 1000 turns with counts
 // (profiles/r05/r05k_board_ab.log): 16^2 0.31 / 0.52, 64^2 0.37 / 0.53, 128^2 0.42 / 0.53,
 // 256^2 0.57 / 0.54, 512^2 0.88 / 0.55.
-constexpr int64_t kBoardAutoRows = 128;
+constexpr int64_t kBoardAutoRows = 256;
 bool stencil_board_shape(int64_t height, int32_t wd, int *W, int *R);
 hipError_t launch_stencil_board(int K, int W, int R, const uint32_t *in_row0, uint32_t *out_row0,
                                 const StencilParams &p, unsigned long long *slots, hipStream_t s);

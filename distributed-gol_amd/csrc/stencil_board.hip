@@ -56,16 +56,35 @@ __device__ __forceinline__ uint32_t unrotate16(uint32_t v, int lane, int K) {
     return __builtin_amdgcn_alignbit(hi, lo, r);
 }
 
-// W waves, R rows per segment: the board has exactly 4 W R rows.  COUNT: per-generation counts into
-// slots[g * kCountSlots] (one slot per generation; count_finalize sums and re-zeroes the slots);
-// LD: the last generation's flips (gol/distributor.go:53-59) into p.diff.
+// wave_sum_dpp of N values at once (the six DPP steps interleaved over the N independent sums)
+template <int N>
+__device__ __forceinline__ void wave_sum_dpp_n(uint32_t (&v)[N]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[i], 0x111, 0xf, 0xf, false);
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[i], 0x112, 0xf, 0xf, false);
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[i], 0x114, 0xf, 0xf, false);
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[i], 0x118, 0xf, 0xf, false);
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[i], 0x142, 0xa, 0xf, false);
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[i], 0x143, 0xc, 0xf, false);
+}
+
+// W waves, R rows per segment: the board has exactly 4 W R rows.  COUNT: generation g's count of
+// wave w into slots[g * kCountSlots + w] with a plain store from one lane (count_finalize sums the
+// slots and re-zeroes them; W <= 16 < kCountSlots).  An LDS atomic per generation compiled to the
+// atomic optimiser's lane loop plus a ds_add on the wave's critical path; the per-generation LDS
+// array also capped K by the LDS size.  LD: the last generation's flips (gol/distributor.go:53-59)
+// into p.diff.
 template <int W, int R, bool COUNT, bool LD>
 __global__ __launch_bounds__(64 * W) void gol_board(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
                                                     StencilParams p, unsigned long long *__restrict__ slots,
                                                     int K) {
     constexpr int NSEG = 4 * W;
     __shared__ uint32_t ex[2][NSEG][4][16];
-    __shared__ uint32_t cnt[COUNT ? kBoardMaxK : 1];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int c16 = lane & 15;
@@ -75,14 +94,12 @@ __global__ __launch_bounds__(64 * W) void gol_board(const uint32_t *__restrict__
     uint32_t c[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) c[r] = in[(int64_t)(sg * R + r) * p.pitch + c16 % wd];
-    if constexpr (COUNT)
-        for (int j = (int)threadIdx.x; j < K; j += 64 * W) cnt[j] = 0u;  // ordered by the first barrier
     const int up = (sg + NSEG - 1) % NSEG, dn = (sg + 1) % NSEG;
     auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
     uint32_t dlast[LD ? R : 1];  // LD: the last generation's flips (drifted frame)
-#pragma clang loop unroll(disable)
-    for (int g = 0; g < K; ++g) {
-        const int par = g & 1;
+    // generation g (exchange buffer par = g & 1): the rows advance in place; returns this lane's
+    // alive cells of the new generation (COUNT)
+    auto gen = [&](int g, int par) -> uint32_t {
         uint32_t s[R], cy[R], ctr[R], nx[R];
         sums16<R>(c, s, cy, ctr);
         ex[par][sg][0][c16] = s[0];
@@ -118,19 +135,43 @@ __global__ __launch_bounds__(64 * W) void gol_board(const uint32_t *__restrict__
             nx[0] = n2[0];
             nx[R - 1] = n2[1];
         }
-        if constexpr (COUNT) {
-            uint32_t a = 0;
+        uint32_t a = 0;
+        if constexpr (COUNT)
 #pragma unroll
             for (int r = 0; r < R; ++r) a += (uint32_t)__builtin_popcount(own ? nx[r] : 0u);
-            a = wave_sum_dpp(a);
-            if (lane == 63 && a) __hip_atomic_fetch_add(&cnt[g], a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
         if constexpr (LD)
             if (g == K - 1)
 #pragma unroll
                 for (int r = 0; r < R; ++r) dlast[r] = nx[r] ^ ctr[r];  // same (new) frame
 #pragma unroll
         for (int r = 0; r < R; ++r) c[r] = nx[r];
+        return a;
+    };
+    // Generations in groups of 4: their four per-wave count reductions (6 dependent DPP adds each)
+    // run interleaved after the group instead of one chain inside every generation.
+    int g = 0;
+#pragma clang loop unroll(disable)
+    for (; g + 4 <= K; g += 4) {
+        uint32_t a[4];
+        a[0] = gen(g, 0);
+        a[1] = gen(g + 1, 1);
+        a[2] = gen(g + 2, 0);
+        a[3] = gen(g + 3, 1);
+        if constexpr (COUNT) {
+            wave_sum_dpp_n<4>(a);
+            if (lane == 63)
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (a[u]) slots[(int64_t)(g + u) * kCountSlots + w] = a[u];  // vector stores (lane 63)
+        }
+    }
+#pragma clang loop unroll(disable)
+    for (; g < K; ++g) {
+        uint32_t a = gen(g, g & 1);
+        if constexpr (COUNT) {
+            a = wave_sum_dpp(a);
+            if (lane == 63 && a) slots[(int64_t)g * kCountSlots + w] = a;
+        }
     }
     // the rows back in the board frame (K bits west around the torus), one copy stored
 #pragma unroll
@@ -141,10 +182,6 @@ __global__ __launch_bounds__(64 * W) void gol_board(const uint32_t *__restrict__
             const uint32_t d = unrotate16(dlast[r], lane, K);
             if (own) p.diff[(int64_t)(sg * R + r) * p.pitch + c16] = d;
         }
-    }
-    if constexpr (COUNT) {
-        __syncthreads();
-        for (int j = (int)threadIdx.x; j < K; j += 64 * W) slots[(int64_t)j * kCountSlots] = cnt[j];
     }
 }
 

@@ -624,7 +624,7 @@ class Engine:
 
     def set_board_kernel(self, enable: int):
         """The whole-board kernel for boards that fit one workgroup (golhip_set_board_kernel): -1
-        automatic (the default: boards of at most 128 rows), 0 / False off, 1 / True every board
+        automatic (the default: boards of at most 256 rows), 0 / False off, 1 / True every board
         it fits."""
         self._check(self._L.golhip_set_board_kernel(self._h, int(enable)))
 

@@ -1,13 +1,14 @@
 """The whole-board kernel (stencil_board.hip, gol_board): boards of 128 / 256 / 512 torus cells per
 row and 4 W R rows run in ONE workgroup for a whole golhip_step call (one launch per 4096
-generations); automatic up to 128 rows, forced here (golhip_set_board_kernel(1)) on taller ones.  Bit-exact against the oracle -- every count of every turn, the board, the last
-generation's flips -- on every (W, R) shape, widths whose torus is replicated (16, 64 cells), calls
-of 1 turn (the flips of a one-generation step), of many generations in one launch, across count
-windows, and against the same engine with the kernel off (the multi-workgroup slabs).
+generations); automatic up to 256 rows, forced here (golhip_set_board_kernel(1)) on taller ones.
+Bit-exact against the oracle -- every count of every turn, the board, the last generation's flips
+-- on every (W, R) shape, widths whose torus is replicated (16, 64 cells), calls of 1 turn (the
+flips of a one-generation step), of many generations in one launch, across count windows, and
+against the same engine with the kernel off (the multi-workgroup slabs).
 
 Reference: server/server.go:21-75 (the rule on a torus), gol/distributor.go:53-59 (flips),
 :153-191 (counts).  The reference's own fixtures (check/images 16/64/512, check/alive CSVs) run
-through this kernel in tests/test_gpu_parity.py, since those boards fit it.
+through this kernel in tests/test_gpu_parity.py where those boards fit its automatic range.
 """
 import numpy as np
 import pytest
@@ -20,8 +21,8 @@ pytestmark = pytest.mark.gpu
 def test_board_kernel_matches_oracle(golhip, oracle, w, h):
     board = (np.random.default_rng(w * 7 + h).random((h, w)) < 0.37).astype(np.uint8) * 255
     with golhip.Engine(w, h, k=16) as e:
-        # automatic up to 128 rows (kBoardAutoRows); forced here for every shape
-        assert (e.launch_kind(16)[0] == "board") == (h <= 128), e.launch_kind(16)
+        # automatic up to 256 rows (kBoardAutoRows); forced here for every shape
+        assert (e.launch_kind(16)[0] == "board") == (h <= 256), e.launch_kind(16)
         e.set_board_kernel(1)
         assert e.launch_kind(16)[0] == "board", e.launch_kind(16)
         e.load(board)
@@ -70,7 +71,7 @@ def test_board_kernel_long_calls_across_count_windows(golhip, oracle):
     _, _, board = oracle.read_pgm(REF / "images/512x512.pgm")
     csv = oracle.read_alive_csv(REF / "check/alive/512x512.csv")
     with golhip.Engine(512, 512, k=16) as e:
-        e.set_board_kernel(1)  # forced (automatic only up to 128 rows)
+        e.set_board_kernel(1)  # forced (automatic only up to 256 rows)
         e.load(board)
         c = e.step(10000, counts=True)
         assert [int(x) for x in c] == [csv[t] for t in range(1, 10001)]

@@ -171,7 +171,7 @@ def test_step_flips_sdl_512_every_count(golhip, oracle):
     with golhip.Engine(512, 512, k=16) as e:
         e.load(board)
         # 512 rows: golhip_step runs this board with the slab kernels (the whole-board kernel is
-        # automatic up to 128 rows); the flips ring with slabs
+        # automatic up to 256 rows); the flips ring with slabs
         assert e.launch_kind(16)[0] == "slab"
         t0 = 0
         for turns in (64, 36):
