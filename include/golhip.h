@@ -259,9 +259,9 @@ int golhip_sync(golhip_t h);                         /* wait for all queued devi
  * to 512 whose lcm with 128 is one of them: the reference's 16/64/128/256/512 sizes) and 4 W R rows
  * (4 ... 512) runs in ONE workgroup holding the whole torus in registers, every golhip_step call as
  * one launch per 4096 generations: no temporal-blocking trapezoid, no halo lanes, no launch
- * boundary inside a call.  enable = -1 (default): boards of at most 128 rows (one CU does the
- * board's whole VALU work per generation: faster than the multi-workgroup slabs up to 128 rows,
- * slower from 256), 1: every board it fits, 0: never (A/B).  golhip_launch_kind reports it as
+ * boundary inside a call.  enable = -1 (default): boards of at most 256 rows (one CU does the
+ * board's whole VALU work per generation: faster than the multi-workgroup slabs up to 256 rows,
+ * slower at 512), 1: every board it fits, 0: never (A/B).  golhip_launch_kind reports it as
  * kind 4 (*param = 100 * waves + rows per segment).  GOLHIP_ERR_ARG outside -1 .. 1. */
 int golhip_set_board_kernel(golhip_t h, int enable);
 /* Stable-slab skipping: the register-slab launches of single-strip boards skip every slab whose
