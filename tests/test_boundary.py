@@ -199,3 +199,17 @@ def test_launch_plan_is_rank_independent_on_uneven_strips(golhip, width, height,
         assert sum(plan) == turns
     if (width, height) == (262144, 262143):
         assert set(golhip.launch_plan(width, height, 16, 160, strips=2)) == {16}
+
+
+def test_register_slab_boards_take_the_fewest_launches(golhip):
+    """Register-slab boards (latency-bound launches, about the same cost at any depth) plan the tail
+    of a call in the fewest launches of the slab depths {16, 12, 8, 4, 2, 1} (slab_first_k): configs[0]
+    (512^2 x 100) is 6 x 16 + 4, not 5 x 16 + 12 + 8 (profiles/r05/r05p_cfg0_timeline.log); boards of
+    at most 256 rows run the whole-board kernel, one launch per call; streaming boards keep the
+    rate-model split (20 turns at 65536^2: 12 + 8)."""
+    assert golhip.launch_plan(512, 512, 16, 100) == [16] * 6 + [4]
+    assert golhip.launch_plan(512, 512, 16, 37) == [16, 16, 4, 1]
+    assert golhip.launch_plan(1000, 600, 16, 46) == [16, 16, 12, 2]
+    assert golhip.launch_plan(256, 256, 16, 100) == [100]
+    assert golhip.launch_plan(4096, 4096, 16, 20) == [16, 4]
+    assert sorted(golhip.launch_plan(65536, 65536, 16, 20)) == [8, 12]
