@@ -605,3 +605,31 @@ def test_counts_pinned_and_device_buffers_interleaved(golhip, oracle):
                 counts = e.step(turns, counts=True)
                 assert np.array_equal(counts.astype(np.int64), oracle.packed_run_words(ref, turns)), (k, turns)
             assert np.array_equal(e.store_words(), ref)
+
+
+def test_short_calls_interleaved_on_a_narrow_board(golhip, oracle):
+    """Short calls on a narrow register-slab board (configs[0]'s shape: packed-slab launches of 16
+    and the tail depths 12 / 8 / 4 / 2, pinned count return): repeated and interleaved calls with and
+    without counts, both buffer parities, a depth change and a count-window change, every count and
+    the board against the oracle, and the turn counter."""
+    words = oracle.init_random(512, 512, seed=77)
+    ref = words.copy()
+    with golhip.Engine(512, 512, k=16) as e:
+        e.load_words(words)
+        turn = 0
+        for turns, counts in [(100, True)] * 4 + [(37, True), (100, False), (37, True), (100, True),
+                                                   (1, True), (1, True), (3, False), (100, True)]:
+            c = e.step(turns, counts=counts)
+            exp = oracle.packed_run_words(ref, turns)
+            if counts:
+                assert np.array_equal(c.astype(np.int64), exp), turns
+            turn += turns
+            assert e.turn == turn
+        e.set_k(12)
+        for _ in range(3):
+            c = e.step(50, counts=True)
+            assert np.array_equal(c.astype(np.int64), oracle.packed_run_words(ref, 50))
+        e.set_count_window(128)
+        c = e.step(100, counts=True)
+        assert np.array_equal(c.astype(np.int64), oracle.packed_run_words(ref, 100))
+        assert np.array_equal(e.store_words(), ref)
