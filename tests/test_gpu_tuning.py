@@ -174,7 +174,9 @@ SLAB_CONFIGS = [(8, 8, 4), (8, 8, 8), (12, 8, 8), (16, 8, 8), (16, 8, 12), (16, 
                 # ... and with every generation's counts flushed at the end (NC = 12)
                 (16, 12, 7, 12), (16, 12, 8, 12), (16, 16, 6, 12), (16, 16, 5, 12),
                 # ... with the younger half of the waves at s_setprio 1 (NC = 13)
-                (16, 16, 6, 13), (16, 12, 7, 13), (16, 8, 12, 13)]
+                (16, 16, 6, 13), (16, 12, 7, 13), (16, 8, 12, 13),
+                # round 5 A/B at 4096^2 with counts: fewer, taller waves (r05t_tune_slab_4096.log)
+                (16, 8, 11, 12), (16, 8, 10, 12), (16, 8, 11, 9), (16, 10, 9, 12)]
 
 
 @pytest.mark.parametrize("cfg", SLAB_CONFIGS)
