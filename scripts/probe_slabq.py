@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""A/B of the persistent counting slab (tuning build, golhip_tuning_step_persistent: one launch
+per 4096-generation count window, neighbour hand-offs instead of launch boundaries) against the
+production path (golhip_step: graph replays of 16-generation gol_slab2 launches), on configs[4]
+(4096^2 glider gun + R-pentomino) and configs[1]'s board (5120^2 random seed 2).  Same board
+and counts required (bit-exact), then us per turn, best of `reps` calls of `turns` turns.
+Usage: probe_slabq.py [turns] [reps]"""
+import ctypes
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "distributed-gol_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401
+
+import golhip  # noqa: E402
+
+turns = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+L = golhip.tuning_library()
+f = L.golhip_tuning_step_persistent
+f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int]
+f.restype = ctypes.c_int
+G = ROOT / "tests" / "golden"
+
+
+def board(n):
+    if n == 4096:
+        b = np.zeros((4096, 4096), dtype=np.uint8)
+        golhip.place(b, golhip.parse_rle((G / "gosper_gun.rle").read_text()), 64, 64)
+        golhip.place(b, golhip.parse_rle((G / "r_pentomino.rle").read_text()), 2048, 2048)
+        return b
+    return None
+
+
+out = {}
+for n, shape in ((4096, 1207), (5120, 1606)):
+    b = board(n)
+    res = {}
+    for mode in ("production", "persistent"):
+        with golhip.Engine(n, n, k=16, lib=L) as e:
+            if b is not None:
+                e.load(b)
+            else:
+                e.init_random(2)
+            counts_all, best = [], 1e9
+            for r in range(reps + 1):
+                c = np.zeros(turns, dtype=np.uint64)
+                e.sync()
+                t = time.perf_counter()
+                if mode == "production":
+                    c = e.step(turns, counts=True)
+                else:
+                    rc = f(e._h, turns, c.ctypes.data, shape)
+                    if rc != 0:
+                        raise RuntimeError(f"persistent rc {rc}: {L.golhip_last_error(e._h).decode()}")
+                e.sync()
+                dt = time.perf_counter() - t
+                counts_all.append(np.asarray(c, dtype=np.uint64).copy())
+                if r > 0:  # the first call captures graphs / warms up
+                    best = min(best, dt)
+            res[mode] = {"us_per_turn": round(best / turns * 1e6, 4), "counts": np.concatenate(counts_all),
+                         "board": e.store_words()}
+    same = bool(np.array_equal(res["production"]["counts"], res["persistent"]["counts"]) and
+                np.array_equal(res["production"]["board"], res["persistent"]["board"]))
+    out[f"{n}_{shape}"] = {"production_us_per_turn": res["production"]["us_per_turn"],
+                           "persistent_us_per_turn": res["persistent"]["us_per_turn"], "bit_exact": same}
+    print(n, shape, out[f"{n}_{shape}"], flush=True)
+print(json.dumps(out))
