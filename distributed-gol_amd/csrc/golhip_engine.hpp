@@ -107,6 +107,9 @@ struct Shard {
     uint32_t *act = nullptr;
     int64_t act_cap = 0;
     unsigned long long *act_stats = nullptr;
+    // golhip_step_persistent: one block counter per slab + the error word
+    uint32_t *pflags = nullptr;
+    int64_t pflags_cap = 0;
 };
 
 struct TimingPair {

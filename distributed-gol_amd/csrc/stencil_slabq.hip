@@ -1,9 +1,12 @@
-// stencil_slabq_tuning.hip -- tuning library only: gol_slabq, a PERSISTENT gol_slab2 (counting, end
-// flush) that runs a whole count window of K-generation blocks in one launch.  Round 5's A/B of
-// DESIGN §3 "Round 5": at configs[1] / configs[4] every slab has its own CU and ~3.3 us of every
+// stencil_slabq.hip -- gol_slabq, a PERSISTENT gol_slab2 (counting, end flush) that runs a whole
+// count window of K-generation blocks in one launch: golhip_step_persistent, an opt-in call
+// (DESIGN §3 "Round 5").  At configs[1] / configs[4] every slab has its own CU and ~3.3 us of every
 // 16-generation launch is its boundary (ramp, row loads, tail); here a slab waits only for the
 // 3 x 3 neighbourhood of slabs (the ones whose rows its next block reads, and that read its
-// rows) to finish the previous block, instead of for a launch boundary.
+// rows) to finish the previous block, instead of for a launch boundary: configs[4]'s board 0.683
+// -> 0.656 us/turn, configs[1]'s 0.755 -> 0.693 (profiles/r05/r05v_persistent_slab_ab.log).
+// Opt-in, not automatic: progress needs every slab resident at once (nothing else on the GPU),
+// and the sc1 hand-off below is MI355X_MICROARCH.md's measured form, not an architectural one.
 //
 // Hand-off (MI355X_MICROARCH.md "Valid forms", table row 1): every store of the board is an `sc1`
 // buffer store, every storing wave waits vmcnt(0), a workgroup barrier, then one lane stores the
@@ -12,8 +15,8 @@
 // grid is one workgroup per slab and the host requires slabs <= CUs, so every workgroup is
 // resident; a poll that waits longer than kSpinTicks sets *err and the workgroup leaves (its
 // neighbours then time out too), so the launch always drains.
-#include "../golhip_engine.hpp"
-#include "../stencil_tile.hpp"
+#include "golhip_engine.hpp"
+#include "stencil_tile.hpp"
 
 namespace golhip {
 namespace {
@@ -239,55 +242,78 @@ using namespace golhip;
 
 extern "C" {
 
-// Tuning library only (not in include/golhip.h): `turns` (a multiple of 16, at most the count
-// window) generations of a single-strip board as ONE launch of the persistent counting slab
-// gol_slabq (W waves x S rows: 1207 / 1606 / 1208), per-turn counts into alive_per_turn.  The
-// slabs must fit the CUs (one resident workgroup each).  Same board and counts as golhip_step.
-int golhip_tuning_step_persistent(golhip_t h, int64_t turns, uint64_t *alive_per_turn, int shape) {
-    if (!h || !alive_per_turn || turns <= 0 || turns % 16 || turns > h->count_window) return GOLHIP_ERR_ARG;
-    if (h->split || h->shards.size() != 1) return fail(h, GOLHIP_ERR_STATE, "persistent slab: single strip only");
-    const int W = shape / 100, S = shape % 100, K = 16;
+// golhip_step_persistent (include/golhip.h): golhip_step with per-turn counts through gol_slabq on
+// single-strip boards whose counting launch is a production gol_slab2 shape with one slab per CU.
+int golhip_step_persistent(golhip_t h, int64_t turns, uint64_t *alive_per_turn) {
+    if (!h || !alive_per_turn || turns < 0) return GOLHIP_ERR_ARG;
+    if (turns == 0) return GOLHIP_OK;
+    constexpr int K = 16;
+    if (h->split || h->shards.size() != 1 || h->k < K || h->variant != kVariantProd)
+        return fail(h, GOLHIP_ERR_STATE, "golhip_step_persistent: a single-strip board of the production kernels, k >= 16");
     Shard &s = h->shards[0];
-    HIPCHK(h, hipSetDevice(s.device));
+    const RegKernel rk = pick_reg_kernel(h, s.rows, K, true);
+    const int shape = rk.kind == 3 && rk.NC == kSlab2E ? rk.W * 100 + rk.S : 0;
+    if (shape != 1207 && shape != 1606 && shape != 1208)
+        return fail(h, GOLHIP_ERR_STATE, "golhip_step_persistent: the board's counting launch is not a gol_slab2 12x7 / 16x6 / 12x8 slab");
     StencilParams q = make_params(h, s, K, 0, s.rows, 0, 0, 0, true);
-    const int T = W * S - 2 * K;
-    if (T < K) return GOLHIP_ERR_ARG;
+    const int T = rk.W * rk.S - 2 * K;
     q.band = T;
     q.band2 = q.nbig0 = 0;
     q.nbands0 = q.nbands = (s.rows + T - 1) / T;
     q.nchunks = (int32_t)((h->wd + kTileChunkWords - 1) / kTileChunkWords);
     const int64_t ngroups = q.nbands * (int64_t)q.nchunks;
-    if (ngroups > h->cus || q.wrap_rows <= 0) return fail(h, GOLHIP_ERR_STATE, "persistent slab: %lld slabs > %d CUs",
-                                                         (long long)ngroups, h->cus);
-    uint32_t *flags = nullptr, *err = nullptr;
-    unsigned long long *dcounts = nullptr;
-    HIPCHK(h, hipMalloc(&flags, sizeof(uint32_t) * (ngroups + 1)));
-    err = flags + ngroups;
-    HIPCHK(h, hipMalloc(&dcounts, sizeof(unsigned long long) * turns));
-    HIPCHK(h, hipMemsetAsync(flags, 0, sizeof(uint32_t) * (ngroups + 1), s.compute));
-    const int nblocks = (int)(turns / K);
-    hipError_t e = hipErrorInvalidValue;
-    uint32_t *b0 = h->row0(s, h->cur), *b1 = h->row0(s, h->cur ^ 1);
-    if (shape == 1207) e = launch_slabq<12, 7>(b0, b1, q, s.slots, flags, nblocks, err, s.compute);
-    if (shape == 1606) e = launch_slabq<16, 6>(b0, b1, q, s.slots, flags, nblocks, err, s.compute);
-    if (shape == 1208) e = launch_slabq<12, 8>(b0, b1, q, s.slots, flags, nblocks, err, s.compute);
-    if (e != hipSuccess) return fail(h, GOLHIP_ERR_HIP, "gol_slabq: %s", hipGetErrorString(e));
-    HIPCHK(h, launch_count_finalize((int)turns, s.slots, dcounts, s.compute));
-    HIPCHK(h, hipStreamSynchronize(s.compute));
+    if (ngroups > h->cus || q.wrap_rows <= 0 || q.nbands < 3)
+        return fail(h, GOLHIP_ERR_STATE, "golhip_step_persistent: %lld slabs (more than the %d CUs, or under 3 bands)",
+                    (long long)ngroups, h->cus);
+    HIPCHK(h, hipSetDevice(s.device));
+    if (s.pflags_cap < ngroups + 1) {
+        SYNCCHK(h, s.compute);
+        if (s.pflags) HIPCHK(h, hipFree(s.pflags));
+        s.pflags = nullptr;
+        s.pflags_cap = 0;
+        HIPCHK(h, hipMalloc(&s.pflags, sizeof(uint32_t) * (ngroups + 1)));
+        s.pflags_cap = ngroups + 1;
+    }
+    if (s.dev_counts_cap < (size_t)turns) {
+        SYNCCHK(h, s.compute);
+        if (s.dev_counts) HIPCHK(h, hipFree(s.dev_counts));
+        s.dev_counts = nullptr;
+        s.dev_counts_cap = 0;
+        HIPCHK(h, hipMalloc(&s.dev_counts, sizeof(unsigned long long) * (size_t)std::max<int64_t>(turns, 128)));
+        s.dev_counts_cap = (size_t)std::max<int64_t>(turns, 128);
+    }
+    uint32_t *const err = s.pflags + ngroups;
+    HIPCHK(h, hipMemsetAsync(err, 0, sizeof(uint32_t), s.compute));
+    // the 16-generation blocks, one launch per count window; a tail under 16 turns: golhip_step
+    const int64_t body = turns / K * K;
+    for (int64_t done = 0; done < body;) {
+        const int64_t n = std::min<int64_t>(body - done, h->count_window / K * K);
+        HIPCHK(h, hipMemsetAsync(s.pflags, 0, sizeof(uint32_t) * ngroups, s.compute));
+        uint32_t *b0 = h->row0(s, h->cur), *b1 = h->row0(s, h->cur ^ 1);
+        const int nblocks = (int)(n / K);
+        hipError_t e = hipErrorInvalidValue;
+        if (shape == 1207) e = launch_slabq<12, 7>(b0, b1, q, s.slots, s.pflags, nblocks, err, s.compute);
+        if (shape == 1606) e = launch_slabq<16, 6>(b0, b1, q, s.slots, s.pflags, nblocks, err, s.compute);
+        if (shape == 1208) e = launch_slabq<12, 8>(b0, b1, q, s.slots, s.pflags, nblocks, err, s.compute);
+        if (e != hipSuccess) return fail(h, GOLHIP_ERR_HIP, "gol_slabq: %s", hipGetErrorString(e));
+        HIPCHK(h, launch_count_finalize((int)n, s.slots, s.dev_counts + done, s.compute));
+        h->cur ^= (nblocks & 1);
+        h->turn += n;
+        done += n;
+    }
+    h->prev_valid = h->diff_valid = h->act_valid = false;
     uint32_t errv = 0;
-    HIPCHK(h, hipMemcpy(&errv, err, sizeof errv, hipMemcpyDeviceToHost));
-    HIPCHK(h, hipMemcpy(alive_per_turn, dcounts, sizeof(uint64_t) * turns, hipMemcpyDeviceToHost));
-    (void)hipFree(flags);
-    (void)hipFree(dcounts);
-    if (errv) return fail(h, GOLHIP_ERR_HIP, "gol_slabq: a neighbour wait timed out");
-    h->cur ^= (nblocks & 1);
-    h->turn += turns;
-    h->prev_valid = false;
-    h->diff_valid = false;
-    h->act_valid = false;
+    HIPCHK(h, hipMemcpyAsync(alive_per_turn, s.dev_counts, sizeof(uint64_t) * (size_t)body, hipMemcpyDeviceToHost,
+                             s.compute));
+    HIPCHK(h, hipMemcpyAsync(&errv, err, sizeof errv, hipMemcpyDeviceToHost, s.compute));
+    SYNCCHK(h, s.compute);
+    if (errv)
+        return fail(h, GOLHIP_ERR_HIP, "golhip_step_persistent: a slab waited over 200 ms for its neighbours (is the GPU "
+                                       "shared?); the board is no longer consistent: reload it");
     const int64_t rep = h->rep();
     if (rep > 1)
-        for (int64_t i = 0; i < turns; ++i) alive_per_turn[i] /= (uint64_t)rep;
+        for (int64_t i = 0; i < body; ++i) alive_per_turn[i] /= (uint64_t)rep;
+    if (body < turns) return run_steps(h, turns - body, alive_per_turn + body, false);
     return GOLHIP_OK;
 }
 

@@ -40,7 +40,7 @@ EXPORTS = [
     "golhip_halo_plan",
     "golhip_create", "golhip_create_strips", "golhip_nccl_unique_id", "golhip_create_rank",
     "golhip_comm_abort", "golhip_edge_wait", "golhip_set_activity", "golhip_activity_stats",
-    "golhip_set_board_kernel",
+    "golhip_set_board_kernel", "golhip_step_persistent",
     "golhip_create_rank_host", "golhip_destroy",
     "golhip_last_error", "golhip_get_info", "golhip_load_bytes", "golhip_init_random",
     "golhip_store_bytes", "golhip_store_words", "golhip_load_words", "golhip_step",
@@ -177,6 +177,7 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
         "golhip_store_words": ([H, ctypes.c_void_p], i32),
         "golhip_load_words": ([H, ctypes.c_void_p], i32),
         "golhip_step": ([H, i64, ctypes.c_void_p], i32),
+        "golhip_step_persistent": ([H, i64, ctypes.c_void_p], i32),
         "golhip_alive_count": ([H, u64p], i32),
         "golhip_alive_cells": ([H, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)], i32),
         "golhip_flips": ([H, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)], i32),
@@ -464,6 +465,13 @@ class Engine:
             return out[:turns]
         self._check(self._L.golhip_step(self._h, turns, None))
         return None
+
+    def step_persistent(self, turns: int) -> np.ndarray:
+        """golhip_step_persistent: `turns` turns with every count, one persistent-slab launch per
+        count window (opt-in; configs[1] / configs[4]-like boards, nothing else on the GPU)."""
+        out = np.zeros(max(turns, 1), dtype=np.uint64)
+        self._check(self._L.golhip_step_persistent(self._h, turns, out.ctypes.data))
+        return out[:turns]
 
     def alive_count(self) -> int:
         v = ctypes.c_uint64()

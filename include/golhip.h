@@ -264,6 +264,15 @@ int golhip_sync(golhip_t h);                         /* wait for all queued devi
  * slower at 512), 1: every board it fits, 0: never (A/B).  golhip_launch_kind reports it as
  * kind 4 (*param = 100 * waves + rows per segment).  GOLHIP_ERR_ARG outside -1 .. 1. */
 int golhip_set_board_kernel(golhip_t h, int enable);
+/* golhip_step with per-turn counts (alive_per_turn non-null) as ONE launch per count window of a
+ * persistent slab kernel (gol_slabq): each slab waits for its 3 x 3 neighbourhood of slabs
+ * through device counters instead of for a launch boundary every 16 generations; the same board
+ * and counts as golhip_step (a tail under 16 turns runs through it).  Opt-in, for single-strip
+ * boards whose counting launch is a gol_slab2 12x7 / 16x6 / 12x8 slab with at most one slab per
+ * CU (configs[1], configs[4]; GOLHIP_ERR_STATE otherwise) and a handle with k >= 16: its progress
+ * needs every slab resident at once, so nothing else may occupy the GPU; a slab that waits over
+ * 200 ms fails the call with GOLHIP_ERR_HIP and leaves the board inconsistent (reload it). */
+int golhip_step_persistent(golhip_t h, int64_t turns, uint64_t *alive_per_turn);
 /* Stable-slab skipping: the register-slab launches of single-strip boards skip every slab whose
  * neighbourhood did not change in the previous launch's last generation -- Life's radius-1 rule
  * keeps such a slab fixed for the launch's K generations -- copying it once and counting its cached

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""A/B of the persistent counting slab (tuning build, golhip_tuning_step_persistent: one launch
+"""A/B of the persistent counting slab (golhip_step_persistent, opt-in: one launch
 per 4096-generation count window, neighbour hand-offs instead of launch boundaries) against the
 production path (golhip_step: graph replays of 16-generation gol_slab2 launches), on configs[4]
 (4096^2 glider gun + R-pentomino) and configs[1]'s board (5120^2 random seed 2).  Same board
@@ -21,10 +21,7 @@ import golhip  # noqa: E402
 
 turns = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-L = golhip.tuning_library()
-f = L.golhip_tuning_step_persistent
-f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int]
-f.restype = ctypes.c_int
+L = golhip.load_library()
 G = ROOT / "tests" / "golden"
 
 
@@ -42,7 +39,7 @@ for n, shape in ((4096, 1207), (5120, 1606)):
     b = board(n)
     res = {}
     for mode in ("production", "persistent"):
-        with golhip.Engine(n, n, k=16, lib=L) as e:
+        with golhip.Engine(n, n, k=16) as e:
             if b is not None:
                 e.load(b)
             else:
@@ -55,9 +52,7 @@ for n, shape in ((4096, 1207), (5120, 1606)):
                 if mode == "production":
                     c = e.step(turns, counts=True)
                 else:
-                    rc = f(e._h, turns, c.ctypes.data, shape)
-                    if rc != 0:
-                        raise RuntimeError(f"persistent rc {rc}: {L.golhip_last_error(e._h).decode()}")
+                    c = e.step_persistent(turns)
                 e.sync()
                 dt = time.perf_counter() - t
                 counts_all.append(np.asarray(c, dtype=np.uint64).copy())

@@ -633,3 +633,50 @@ def test_short_calls_interleaved_on_a_narrow_board(golhip, oracle):
         c = e.step(100, counts=True)
         assert np.array_equal(c.astype(np.int64), oracle.packed_run_words(ref, 100))
         assert np.array_equal(e.store_words(), ref)
+
+
+@pytest.mark.parametrize("case", ["configs4", "configs1"])
+def test_persistent_slab_matches_oracle(golhip, oracle, case):
+    """golhip_step_persistent (gol_slabq: a whole count window of 16-generation blocks in ONE
+    launch, each slab waiting for its 3 x 3 neighbourhood through sc1 counters instead of a launch
+    boundary): configs[4]'s board (4096^2 gun + R-pentomino, 12 x 7 slabs, a short last band: 4096 =
+    78 x 52 + 40) and configs[1]'s (5120^2 random, 16 x 6); calls of 16 turns, of more than one count
+    window (4096 + 512, the count window shrunk to 4096 / 8 for the second engine), a tail under 16
+    turns; every count and the board against the oracle; interleaved with golhip_step."""
+    from conftest import GOLDEN
+
+    if case == "configs4":
+        n = 4096
+        board = np.zeros((n, n), dtype=np.uint8)
+        golhip.place(board, golhip.parse_rle((GOLDEN / "gosper_gun.rle").read_text()), 64, 64)
+        golhip.place(board, golhip.parse_rle((GOLDEN / "r_pentomino.rle").read_text()), 2048, 2048)
+        code = 121207
+    else:
+        n = 5120
+        board = oracle.unpack(oracle.init_random(n, n, seed=2), n)
+        code = 121606
+    ref = board.copy()
+    with golhip.Engine(n, n, k=16) as e:
+        assert e.launch_kind(16, counts=True) == ("slab", code)
+        e.load(board)
+        if case == "configs1":
+            e.set_count_window(512)
+        turn = 0
+        for turns, persistent in ((16, True), (600, True), (37, False), (1043, True)):
+            c = e.step_persistent(turns) if persistent else e.step(turns, counts=True)
+            ref, exp = oracle.packed_run(ref, turns)
+            assert np.array_equal(c.astype(np.int64), exp), (case, turns)
+            turn += turns
+            assert e.turn == turn
+        assert np.array_equal(e.store(), ref)
+
+
+def test_persistent_slab_refuses_other_boards(golhip):
+    """Boards whose counting launch is not a one-round gol_slab2 slab: GOLHIP_ERR_STATE, no
+    device work."""
+    for (w, h) in [(512, 512), (65536, 1024), (16384, 16384)]:
+        with golhip.Engine(w, h, k=16) as e:
+            e.init_random(1)
+            with pytest.raises(golhip.GolHipError):
+                e.step_persistent(32)
+            assert e.turn == 0

@@ -337,28 +337,3 @@ def test_stamp_variant_k1_then_deep(golhip, tuning, monkeypatch):
         well_formed(*_stamps(tuning, e))
         assert bench.board_digest(e.store_words(), 1) == d1008
 
-
-def test_persistent_slab_matches_production(golhip, tuning, oracle):
-    """gol_slabq (tuning build, golhip_tuning_step_persistent): a whole count window of 16-generation
-    blocks in ONE launch, each slab waiting for its 3 x 3 neighbourhood through sc1 counters
-    instead of a launch boundary.  Every count and the board against the oracle, on a board with a
-    short last band (1000 rows = 19 x 52 + 12 at 12 x 7) and one of 2 chunks, and calls of 16 and
-    of 1024 turns."""
-    import ctypes
-
-    f = tuning.golhip_tuning_step_persistent
-    f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int]
-    f.restype = ctypes.c_int
-    for (h, w, shape) in [(1000, 2048, 1207), (640, 4096, 1606), (1040, 1024, 1208)]:
-        rng = np.random.default_rng(h + w)
-        board = ((rng.random((h, w)) < 0.35) * 255).astype(np.uint8)
-        ref = board.copy()
-        with golhip.Engine(w, h, k=16, lib=tuning) as e:
-            e.load(board)
-            for turns in (16, 1024, 48):
-                c = np.zeros(turns, dtype=np.uint64)
-                assert f(e._h, turns, c.ctypes.data, shape) == 0, tuning.golhip_last_error(e._h)
-                ref, exp = oracle.packed_run(ref, turns)
-                assert np.array_equal(c.astype(np.int64), exp), (h, w, shape, turns)
-            assert np.array_equal(e.store(), ref)
-            assert e.turn == 16 + 1024 + 48
