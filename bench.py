@@ -584,6 +584,22 @@ def configs_leg() -> dict:
 
     runs, runs_sorted, ok, kind, stats = cfg2_runs(-1)
     runs_d, runs_dsorted, ok_d, _, stats_d = cfg2_runs(1)
+
+    def persistent_runs(setup, turns, exp, nruns):  # golhip_step_persistent (opt-in), A/B
+        with golhip.Engine(setup[0], setup[0], k=16) as e:
+            setup[1](e)
+            e.step_persistent(4096)  # warm
+            ts, okp = [], True
+            for _ in range(nruns):
+                setup[1](e)
+                e.sync()
+                t = time.perf_counter()
+                c = e.step_persistent(turns)
+                ts.append(time.perf_counter() - t)
+                okp = okp and bool(np.array_equal(c.astype(np.uint64), exp))
+        return min(ts), okp
+
+    dt_p2, ok_p2 = persistent_runs((5120, lambda e: e.init_random(2)), 10000, exp2, 3)
     dt = runs_sorted[len(runs_sorted) // 2]
     dt_d = runs_dsorted[len(runs_dsorted) // 2]
     res["cfg2_5120x10000"] = {"us_per_turn": round(dt / 10000 * 1e6, 3),
@@ -594,7 +610,11 @@ def configs_leg() -> dict:
                               "stable_slab_skipping": {"slabs_computed": stats[0], "slabs_skipped": stats[1]},
                               "skipping_forced": {"us_per_turn": round(dt_d / 10000 * 1e6, 3),
                                                   "gcups": round(5120 * 5120 * 10000 / dt_d / 1e9, 1),
-                                                  "slabs_computed": stats_d[0], "slabs_skipped": stats_d[1]}}
+                                                  "slabs_computed": stats_d[0], "slabs_skipped": stats_d[1]},
+                              # golhip_step_persistent: one launch per count window (opt-in: needs
+                              # the GPU to itself), best of 3, every count checked
+                              "persistent_opt_in": {"us_per_turn": round(dt_p2 / 10000 * 1e6, 3),
+                                                    "counts_match_all_10000": ok_p2}}
     # configs[4]
     b = np.zeros((4096, 4096), dtype=np.uint8)
     golhip.place(b, golhip.parse_rle((GOLDEN / "gosper_gun.rle").read_text()), 64, 64)
@@ -618,6 +638,7 @@ def configs_leg() -> dict:
 
     dt, ok5, kind, stats = cfg5_run(-1)
     dt_d, ok5_d, _, stats_d = cfg5_run(1)
+    dt_p5, ok_p5 = persistent_runs((4096, lambda e: e.load(b)), 1000000, exp5, 1)
     res["cfg5_4096x1e6"] = {"us_per_turn": round(dt, 3), "gcups": round(4096 * 4096 * 1e6 / dt / 1e9, 1),
                             "counts_match_all_1e6": bool(ok5 and ok5_d),
                             "kernel": f"{kind[0]}{kind[1] or ''}",
@@ -626,10 +647,12 @@ def configs_leg() -> dict:
                             # long as its slowest computed slab: 237 slabs, one per CU)
                             "skipping_forced": {"us_per_turn": round(dt_d, 3),
                                                 "gcups": round(4096 * 4096 * 1e6 / dt_d / 1e9, 1),
-                                                "slabs_computed": stats_d[0], "slabs_skipped": stats_d[1]}}
+                                                "slabs_computed": stats_d[0], "slabs_skipped": stats_d[1]},
+                            "persistent_opt_in": {"us_per_turn": round(dt_p5, 3),
+                                                  "counts_match_all_1e6": ok_p5}}
     res["ok"] = bool(res["cfg1_512x100"]["bit_exact_vs_reference_fixture"]
-                     and res["cfg2_5120x10000"]["counts_match_all_10000"]
-                     and res["cfg5_4096x1e6"]["counts_match_all_1e6"])
+                     and res["cfg2_5120x10000"]["counts_match_all_10000"] and ok_p2
+                     and res["cfg5_4096x1e6"]["counts_match_all_1e6"] and ok_p5)
     return res
 
 
