@@ -3,8 +3,8 @@
 // (DESIGN §3 "Round 5").  At configs[1] / configs[4] every slab has its own CU and ~3.3 us of every
 // 16-generation launch is its boundary (ramp, row loads, tail); here a slab waits only for the
 // 3 x 3 neighbourhood of slabs (the ones whose rows its next block reads, and that read its
-// rows) to finish the previous block, instead of for a launch boundary: configs[4]'s board 0.683
-// -> 0.656 us/turn, configs[1]'s 0.755 -> 0.693 (profiles/r05/r05v_persistent_slab_ab.log).
+// rows) to finish the previous block, instead of for a launch boundary: configs[4]'s board 0.682
+// -> 0.644 us/turn, configs[1]'s 0.755 -> 0.698 (profiles/r05/r05w_persistent_slab.log).
 // Opt-in, not automatic: progress needs every slab resident at once (nothing else on the GPU),
 // and the sc1 hand-off below is MI355X_MICROARCH.md's measured form, not an architectural one.
 //
