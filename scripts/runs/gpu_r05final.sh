@@ -2,7 +2,7 @@
 # round 5 (final): GPU suite, smoke, the default and driver-shaped bench lines, and rocprofv3
 # kernel stats of the default bench command (the line under rocprof beside it)
 set -u
-O=gpurun_out/r05final
+O=gpurun_out/${R05_OUT:-r05final}
 mkdir -p $O
 export TMPDIR=/tmp
 G=scripts/guard.sh
