@@ -250,6 +250,8 @@ int golhip_step_persistent(golhip_t h, int64_t turns, uint64_t *alive_per_turn) 
     constexpr int K = 16;
     if (h->split || h->shards.size() != 1 || h->k < K || h->variant != kVariantProd)
         return fail(h, GOLHIP_ERR_STATE, "golhip_step_persistent: a single-strip board of the production kernels, k >= 16");
+    if (h->track_flips)  // gol_slabq writes no flips board
+        return fail(h, GOLHIP_ERR_STATE, "golhip_step_persistent: flip tracking is on (use golhip_step)");
     Shard &s = h->shards[0];
     const RegKernel rk = pick_reg_kernel(h, s.rows, K, true);
     const int shape = rk.kind == 3 && rk.NC == kSlab2E ? rk.W * 100 + rk.S : 0;

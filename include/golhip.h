@@ -269,7 +269,8 @@ int golhip_set_board_kernel(golhip_t h, int enable);
  * through device counters instead of for a launch boundary every 16 generations; the same board
  * and counts as golhip_step (a tail under 16 turns runs through it).  Opt-in, for single-strip
  * boards whose counting launch is a gol_slab2 12x7 / 16x6 / 12x8 slab with at most one slab per
- * CU (configs[1], configs[4]; GOLHIP_ERR_STATE otherwise) and a handle with k >= 16: its progress
+ * CU (configs[1], configs[4]; GOLHIP_ERR_STATE otherwise), a handle with k >= 16 and flip
+ * tracking off (golhip_track_flips: GOLHIP_ERR_STATE, use golhip_step): its progress
  * needs every slab resident at once, so nothing else may occupy the GPU; a slab that waits over
  * 200 ms fails the call with GOLHIP_ERR_HIP and leaves the board inconsistent (reload it). */
 int golhip_step_persistent(golhip_t h, int64_t turns, uint64_t *alive_per_turn);

@@ -680,3 +680,13 @@ def test_persistent_slab_refuses_other_boards(golhip):
             with pytest.raises(golhip.GolHipError):
                 e.step_persistent(32)
             assert e.turn == 0
+    # a board it takes, but with flip tracking on (gol_slabq writes no flips board)
+    with golhip.Engine(4096, 4096, k=16) as e:
+        e.init_random(1)
+        e.track_flips(True)
+        with pytest.raises(golhip.GolHipError, match="flip tracking"):
+            e.step_persistent(32)
+        assert e.turn == 0
+        e.track_flips(False)
+        e.step_persistent(32)
+        assert e.turn == 32
