@@ -4,7 +4,8 @@ us per turn of golhip_step for each forced gol_slab shape (GOLHIP_SLAB = NC*1000
 K = 16), with and without per-turn counts, median of 3 interleaved rounds.  Every shape's
 per-turn counts must equal the golden (5120^2 seed 2: tests/golden cfg2 CSV) or, on other
 sizes, the automatic shape's counts.
-Usage: tune_slab.py size[,size..] shape[,shape..] [turns]   (shape 0 = automatic choice)"""
+Usage: tune_slab.py size[,size..] shape[,shape..] [turns]   (shape 0 = automatic choice; a size
+is N for N x N or WxH)"""
 import json
 import os
 import statistics
@@ -21,14 +22,15 @@ import torch  # noqa: E402,F401
 
 import golhip  # noqa: E402
 
-sizes = [int(x) for x in sys.argv[1].split(",")]
+sizes = sys.argv[1].split(",")
 shapes = [int(x) for x in sys.argv[2].split(",")]
 turns = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
 gold = json.loads((ROOT / "tests/golden/synthetic_golden.json").read_text())
 res, ok = {}, {}
 for n in sizes:
+    w, h = (int(v) for v in n.split("x")) if "x" in n else (int(n), int(n))
     ref = None
-    if n == 5120:
+    if n == "5120":
         lines = (ROOT / "tests/golden" / gold["cfg2"]["counts_csv"]).read_text().split()[1:]
         ref = np.array([int(ln.split(",")[1]) for ln in lines[:256 + turns]], dtype=np.uint64)
     engines = {}
@@ -37,7 +39,7 @@ for n in sizes:
             os.environ["GOLHIP_SLAB"] = str(sh)
         else:
             os.environ.pop("GOLHIP_SLAB", None)
-        engines[sh] = golhip.Engine(n, n, k=16)
+        engines[sh] = golhip.Engine(w, h, k=16)
     os.environ.pop("GOLHIP_SLAB", None)
     for rnd in range(3):
         for sh, e in engines.items():
