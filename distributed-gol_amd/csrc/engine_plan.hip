@@ -295,11 +295,16 @@ RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K, bool counting) 
     // (NC = 12): the per-barrier flush sat on each generation's critical path -- 5120^2 16 x 6
     // 0.852 -> 0.772 us/turn, 4096^2 12 x 7 0.782 -> 0.730 (profiles/r04/r04u_tune.log; moving
     // the 8 x 12 flush INTO the loop instead cost 0.844 -> 0.945, r04t).
-    static constexpr Cand kCount16[] = {{16, 6, 12}, {8, 12, 9}, {12, 8, 12}, {12, 7, 12}};
-    static constexpr Cand kPlain16[] = {{16, 6, 9}, {12, 8, 9}, {8, 12, 9}, {12, 7, 9}};
+    // Round 5: 16 x 4 (T = 32, 16 rows per SIMD) for boards whose 16 x 4 slabs fit one round over
+    // the CUs, e.g. two-chunk widths at 4096 rows: 3968 x 4096 with every count 0.706 (12 x 7,
+    // 158 slabs) -> 0.583 us/turn (256 slabs), without counts 0.659 -> 0.543; 12 x 6 0.652, 16 x 5
+    // 0.654 (profiles/r05/r05y_rows_per_cu_ab.log).  The rows-per-SIMD model orders all four; 16 x 4
+    // is a candidate only in one round (larger boards keep the taller slabs' lower halo share).
+    static constexpr Cand kCount16[] = {{16, 6, 12}, {8, 12, 9}, {12, 8, 12}, {12, 7, 12}, {16, 4, 12}};
+    static constexpr Cand kPlain16[] = {{16, 6, 9}, {12, 8, 9}, {8, 12, 9}, {12, 7, 9}, {16, 4, 9}};
     static constexpr Cand kOther[] = {{8, 8, 4}};
     const Cand *cands = K == 16 ? (counting ? kCount16 : kPlain16) : kOther;
-    const int ncand = K == 16 ? 4 : 1;
+    const int ncand = K == 16 ? 5 : 1;
     double best = 1e300;
     for (int i = 0; i < ncand; ++i) {
         const Cand c = cands[i];
@@ -308,6 +313,7 @@ RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K, bool counting) 
         if (T < 1) continue;
         const int64_t slabs = (rows_total + T - 1) / T * ((h->wd + kTileChunkWords - 1) / kTileChunkWords);
         const int64_t rounds = (slabs + cus - 1) / cus;
+        if (c.S == 4 && rounds > 1) continue;  // 16 x 4: measured in one round only
         const double cost = (double)rounds * (double)((c.W + 3) / 4) * c.S;
         if (cost < best) {  // ties keep the earlier (measured-preferred) shape
             best = cost;

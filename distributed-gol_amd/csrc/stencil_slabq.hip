@@ -255,8 +255,9 @@ int golhip_step_persistent(golhip_t h, int64_t turns, uint64_t *alive_per_turn) 
     Shard &s = h->shards[0];
     const RegKernel rk = pick_reg_kernel(h, s.rows, K, true);
     const int shape = rk.kind == 3 && rk.NC == kSlab2E ? rk.W * 100 + rk.S : 0;
-    if (shape != 1207 && shape != 1606 && shape != 1208)
-        return fail(h, GOLHIP_ERR_STATE, "golhip_step_persistent: the board's counting launch is not a gol_slab2 12x7 / 16x6 / 12x8 slab");
+    if (shape != 1207 && shape != 1606 && shape != 1208 && shape != 1604)
+        return fail(h, GOLHIP_ERR_STATE,
+                    "golhip_step_persistent: the board's counting launch is not a gol_slab2 12x7 / 16x6 / 12x8 / 16x4 slab");
     StencilParams q = make_params(h, s, K, 0, s.rows, 0, 0, 0, true);
     const int T = rk.W * rk.S - 2 * K;
     q.band = T;
@@ -297,6 +298,7 @@ int golhip_step_persistent(golhip_t h, int64_t turns, uint64_t *alive_per_turn) 
         if (shape == 1207) e = launch_slabq<12, 7>(b0, b1, q, s.slots, s.pflags, nblocks, err, s.compute);
         if (shape == 1606) e = launch_slabq<16, 6>(b0, b1, q, s.slots, s.pflags, nblocks, err, s.compute);
         if (shape == 1208) e = launch_slabq<12, 8>(b0, b1, q, s.slots, s.pflags, nblocks, err, s.compute);
+        if (shape == 1604) e = launch_slabq<16, 4>(b0, b1, q, s.slots, s.pflags, nblocks, err, s.compute);
         if (e != hipSuccess) return fail(h, GOLHIP_ERR_HIP, "gol_slabq: %s", hipGetErrorString(e));
         HIPCHK(h, launch_count_finalize((int)n, s.slots, s.dev_counts + done, s.compute));
         h->cur ^= (nblocks & 1);

@@ -19,7 +19,7 @@ namespace golhip {
 // packed launch: profiles/r05/r05p_cfg0_timeline.log).
 #define GOLHIP_SLAB_PROD_CONFIGS(X) \
     X(8, 8, 8, 4) X(12, 8, 8, 4) X(16, 8, 12, 9) X(16, 16, 6, 9) X(16, 12, 8, 9) X(16, 12, 7, 9) \
-    X(16, 16, 6, 12) X(16, 12, 7, 12) X(16, 12, 8, 12) X(16, 4, 3, 14) X(16, 6, 3, 14) X(16, 8, 3, 14) \
+    X(16, 16, 6, 12) X(16, 12, 7, 12) X(16, 12, 8, 12) X(16, 16, 4, 9) X(16, 16, 4, 12) X(16, 4, 3, 14) X(16, 6, 3, 14) X(16, 8, 3, 14) \
     X(12, 4, 3, 14) X(12, 6, 3, 14) X(12, 8, 3, 14) X(8, 4, 3, 14) X(8, 6, 3, 14) X(8, 8, 3, 14) \
     X(4, 4, 3, 14) X(4, 6, 3, 14) X(4, 8, 3, 14) X(2, 4, 3, 14) X(2, 6, 3, 14) X(2, 8, 3, 14)
 

@@ -1359,7 +1359,8 @@ constexpr int kSlab2P = 13;  // gol_slab2 FM = 2 with the younger half of the wa
 constexpr int kSlabP = 14;  // gol_slabp: P = 64 / (wd + 2) row segments packed per wave (wd <= 62)
 constexpr bool slab_prod_ws(int K, int W, int S) {
     return (K == 16 && W == 8 && S == 12) || (K == 16 && W == 12 && S == 8) ||
-           (K == 16 && W == 12 && S == 7) || (K == 16 && W == 16 && S == 6) || (K == 8 && W == 8 && S == 8) ||
+           (K == 16 && W == 12 && S == 7) || (K == 16 && W == 16 && S == 6) || (K == 16 && W == 16 && S == 4) ||
+           (K == 8 && W == 8 && S == 8) ||
            (K == 12 && W == 8 && S == 8) ||
            ((K == 16 || K == 12 || K == 8 || K == 4 || K == 2) && S == 3 && (W == 4 || W == 6 || W == 8));
 }

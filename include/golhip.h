@@ -268,7 +268,7 @@ int golhip_set_board_kernel(golhip_t h, int enable);
  * persistent slab kernel (gol_slabq): each slab waits for its 3 x 3 neighbourhood of slabs
  * through device counters instead of for a launch boundary every 16 generations; the same board
  * and counts as golhip_step (a tail under 16 turns runs through it).  Opt-in, for single-strip
- * boards whose counting launch is a gol_slab2 12x7 / 16x6 / 12x8 slab with at most one slab per
+ * boards whose counting launch is a gol_slab2 12x7 / 16x6 / 12x8 / 16x4 slab with at most one slab per
  * CU (configs[1], configs[4]; GOLHIP_ERR_STATE otherwise), a handle with k >= 16 and flip
  * tracking off (golhip_track_flips: GOLHIP_ERR_STATE, use golhip_step): its progress
  * needs every slab resident at once, so nothing else may occupy the GPU; a slab that waits over

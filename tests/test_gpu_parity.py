@@ -482,6 +482,34 @@ def test_small_board_picks_register_slab(golhip, oracle):
     assert np.array_equal(counts.astype(np.int64), ref_counts)
 
 
+def test_two_chunk_board_takes_16x4_slabs(golhip, oracle):
+    """A board of two 62-word chunks at 4096 rows (3968 x 4096: 124 packed words) fits 16 x 4 slabs
+    (T = 32, 256 slabs) in one round over the CUs, 16 rows per SIMD against 12 x 7's 21
+    (pick_reg_kernel, round 5): every count and the board against the oracle through golhip_step
+    with and without counts and through golhip_step_persistent."""
+    w, h = 3968, 4096
+    board = oracle.unpack(oracle.init_random(w, h, seed=7), w)
+    ref = board.copy()
+    import torch
+
+    if torch.cuda.get_device_properties(0).multi_processor_count < 256:
+        pytest.skip("the 16 x 4 choice needs 256 CUs for this board")
+    with golhip.Engine(w, h, k=16) as e:
+        assert e.launch_kind(16) == ("slab", 91604)
+        assert e.launch_kind(16, counts=True) == ("slab", 121604)
+        e.load(board)
+        c = e.step(300, counts=True)
+        ref, exp = oracle.packed_run(ref, 300)
+        assert np.array_equal(c.astype(np.int64), exp)
+        e.step(133)
+        ref, _ = oracle.packed_run(ref, 133)
+        assert np.array_equal(e.store(), ref)
+        c = e.step_persistent(261)
+        ref, exp = oracle.packed_run(ref, 261)
+        assert np.array_equal(c.astype(np.int64), exp)
+        assert np.array_equal(e.store(), ref)
+
+
 @pytest.mark.parametrize("stage", [0, 4096])
 @pytest.mark.parametrize("shape", [(512, 512), (300, 1000), (96, 640), (40, 6)])
 def test_store_interleaved_with_steps(golhip, oracle, monkeypatch, tmp_path, stage, shape):
