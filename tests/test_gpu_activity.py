@@ -62,12 +62,13 @@ def run_engine(golhip, board, k, calls, activity=True, graphs=-1, counts=True):
 @pytest.mark.parametrize("h,w,calls,graphs", [
     (4096, 4096, [300, 700, 1000], -1),   # configs[4]-sized slabs (12 x 7 with counts)
     (5120, 5120, [640, 640], 1),          # 16 x 6, graph replays of 128-generation blocks
-    (2048, 1152, [512, 33, 455], -1),     # 9 column chunks; tails of other depths between
+    (2048, 1152, [512, 33, 455], -1),     # 16 x 4 slabs; tails of other depths between
     (1000, 600, [384, 128], 0),           # width not a multiple of 128 (torus replicated 32 times:
                                           # every object is in every chunk of its band, so only 3
-                                          # objects), no graphs, a last band of 12 < K rows
-                                          # (1000 = 19 x 52 + 12)
-    (3072, 3072, [512], -1),              # last band 4 rows (3072 = 59 x 52 + 4)
+                                          # objects), no graphs, a last band of 8 < K rows
+                                          # (16 x 4 slabs: 1000 = 31 x 32 + 8)
+    (3076, 3072, [512], -1),              # last band 4 rows (16 x 4 slabs: 3076 = 96 x 32 + 4)
+    (4164, 4096, [512], -1),              # last band 4 rows (12 x 7 slabs: 4164 = 80 x 52 + 4)
 ])
 def test_sparse_boards_match_oracle(golhip, oracle, h, w, calls, graphs):
     board = sparse_board(h, w, seed=h + w, **({} if w % 128 == 0 else dict(n_gliders=1, n_osc=1, n_still=1)))
@@ -82,10 +83,10 @@ def test_sparse_boards_match_oracle(golhip, oracle, h, w, calls, graphs):
 def test_skipping_on_and_off_identical_without_counts_then_with(golhip, oracle):
     """Non-counting and counting launches (their slab kernels differ, same geometry or not) in one
     handle, skipping on vs off: the same board, the same counts."""
-    board = sparse_board(3072, 3072, seed=5, n_gliders=12)
+    board = sparse_board(3076, 3072, seed=5, n_gliders=12)
     outs = []
     for act in (True, False):
-        with golhip.Engine(3072, 3072, k=16) as e:
+        with golhip.Engine(3072, 3076, k=16) as e:
             e.set_activity(act)
             e.load(board)
             e.step(400)
@@ -95,7 +96,7 @@ def test_skipping_on_and_off_identical_without_counts_then_with(golhip, oracle):
             outs.append((e.store(), c1, c2, e.activity_stats()))
     assert np.array_equal(outs[0][0], outs[1][0])
     assert np.array_equal(outs[0][1], outs[1][1]) and np.array_equal(outs[0][2], outs[1][2])
-    assert outs[0][3][1] > 0 and outs[1][3] == (0, 0), (outs[0][3], outs[1][3])  # 3072 = 59 x 52 + 4
+    assert outs[0][3][1] > 0 and outs[1][3] == (0, 0), (outs[0][3], outs[1][3])  # 3076 = 96 x 32 + 4
     ref, ref_counts = oracle.packed_run(board, 1100)
     assert np.array_equal(outs[0][0], ref)
     assert np.array_equal(outs[0][2].astype(np.int64), ref_counts[-271:])
