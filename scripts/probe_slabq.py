@@ -4,7 +4,8 @@ per 4096-generation count window, neighbour hand-offs instead of launch boundari
 production path (golhip_step: graph replays of 16-generation gol_slab2 launches), on configs[4]
 (4096^2 glider gun + R-pentomino) and configs[1]'s board (5120^2 random seed 2).  Same board
 and counts required (bit-exact), then us per turn, best of `reps` calls of `turns` turns.
-Usage: probe_slabq.py [turns] [reps]"""
+Usage: probe_slabq.py [turns] [reps] [boards]   (boards: N or WxH, comma-separated; default
+4096,5120; 4096 is configs[4]'s board, the others random seed 2)"""
 import ctypes
 import json
 import os
@@ -21,12 +22,13 @@ import golhip  # noqa: E402
 
 turns = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+boards = (sys.argv[3] if len(sys.argv) > 3 else "4096,5120").split(",")
 L = golhip.load_library()
 G = ROOT / "tests" / "golden"
 
 
 def board(n):
-    if n == 4096:
+    if n == "4096":
         b = np.zeros((4096, 4096), dtype=np.uint8)
         golhip.place(b, golhip.parse_rle((G / "gosper_gun.rle").read_text()), 64, 64)
         golhip.place(b, golhip.parse_rle((G / "r_pentomino.rle").read_text()), 2048, 2048)
@@ -35,11 +37,13 @@ def board(n):
 
 
 out = {}
-for n, shape in ((4096, 1207), (5120, 1606)):
+for n in boards:
+    w, h = (int(v) for v in n.split("x")) if "x" in n else (int(n), int(n))
     b = board(n)
     res = {}
     for mode in ("production", "persistent"):
-        with golhip.Engine(n, n, k=16) as e:
+        with golhip.Engine(w, h, k=16) as e:
+            shape = e.launch_kind(16, counts=True)[1]
             if b is not None:
                 e.load(b)
             else:
