@@ -17,7 +17,7 @@ namespace {
     X(16, 8, 12, 10) X(16, 16, 6, 10) X(16, 12, 8, 10) X(16, 12, 7, 10) X(16, 10, 8, 10) X(16, 8, 10, 10) \
     X(16, 8, 12, 11) X(16, 8, 10, 11) X(16, 10, 8, 11) X(16, 12, 8, 11) \
     X(16, 16, 5, 12) X(16, 16, 6, 13) X(16, 12, 7, 13) X(16, 8, 12, 13) \
-    X(16, 8, 11, 12) X(16, 8, 10, 12) X(16, 8, 11, 9) X(16, 10, 9, 12) X(16, 12, 6, 12) X(16, 16, 4, 12) \
+    X(16, 8, 11, 12) X(16, 8, 10, 12) X(16, 8, 11, 9) X(16, 10, 9, 12) X(16, 12, 6, 12) X(16, 16, 4, 12) X(16, 8, 6, 12) X(16, 12, 4, 12) \
     X(16, 4, 4, 14) X(16, 8, 4, 14) X(16, 8, 6, 14) X(16, 16, 3, 14) \
     X(16, 4, 5, 14) X(16, 4, 6, 14) X(16, 12, 3, 14) X(16, 2, 6, 14) X(16, 2, 8, 14) \
     X(12, 8, 3, 14) X(12, 4, 3, 14) X(8, 8, 3, 14) X(8, 4, 3, 14) X(8, 4, 4, 14)
