@@ -82,6 +82,111 @@ _HWQ = _hw_queues(sys.argv[1:])
 if _HWQ > 0:
     os.environ["GPU_MAX_HW_QUEUES"] = str(max(_HWQ, int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0)))
 
+
+def _argv_int(argv, name: str, default: int) -> int:
+    """--name N / --name=N from argv, read before argparse (and before torch is imported)."""
+    for i, x in enumerate(argv):
+        if x == name and i + 1 < len(argv):
+            return int(argv[i + 1])
+        if x.startswith(name + "="):
+            return int(x.split("=", 1)[1])
+    return default
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(argv, n: int, deadline_s: float, script: str | None = None) -> int:
+    """`python bench.py --gpus N ...` run plainly (no torch.distributed.run, WORLD_SIZE unset): start
+    the N rank processes of one node here and wait for them -- the broker bringing up its own
+    server connections (broker/broker.go:191-205) instead of expecting them to exist.
+
+    Runs before this process imports torch or loads libgolhip, so it never initialises the GPU and
+    never exec()s: each rank is a fresh child (`sys.executable bench.py <same args>`) with the
+    environment torch.distributed.run would give it (RANK, LOCAL_RANK, WORLD_SIZE,
+    LOCAL_WORLD_SIZE, MASTER_ADDR 127.0.0.1, a free MASTER_PORT).  Rank 0's JSON line is relayed
+    to stdout as this command's one line; everything else the ranks print goes to stderr.  Returns the exit code: 0 only if
+    every rank exited 0; when a rank fails, the others get a grace period (their own collective
+    deadlines fire first) and are then terminated; at the deadline every rank is killed."""
+    import signal
+    import subprocess
+    import threading
+
+    script = script or os.path.abspath(__file__)
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   GOLHIP_BENCH_LAUNCHER=str(os.getpid()))
+        procs.append(subprocess.Popen([sys.executable, "-u", script, *argv], env=env, start_new_session=True,
+                                      stdout=subprocess.PIPE, bufsize=0))
+
+    def relay(r, pipe):  # rank 0's JSON line -> stdout; everything else a rank prints -> stderr
+        for raw in iter(pipe.readline, b""):
+            to = sys.stdout if r == 0 and raw.lstrip().startswith(b"{") else sys.stderr
+            to.buffer.write(raw)
+            to.flush()
+
+    relays = [threading.Thread(target=relay, args=(r, p.stdout), daemon=True) for r, p in enumerate(procs)]
+    for t in relays:
+        t.start()
+    print(f"bench: launched {n} rank processes (pids {[p.pid for p in procs]}), master 127.0.0.1:{port}",
+          file=sys.stderr, flush=True)
+    t_end = time.monotonic() + deadline_s
+    first_fail = None
+
+    def stop(sig):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, sig)
+                except ProcessLookupError:
+                    pass
+
+    try:
+        while any(p.poll() is None for p in procs):
+            now = time.monotonic()
+            failed = [i for i, p in enumerate(procs) if p.returncode not in (None, 0)]
+            if failed and first_fail is None:
+                first_fail = now
+                print(f"bench: rank(s) {failed} exited {[procs[i].returncode for i in failed]}; "
+                      f"stopping the others in 15 s", file=sys.stderr, flush=True)
+            if now > t_end or (first_fail is not None and now > first_fail + 15):
+                stop(signal.SIGTERM)
+                try:
+                    for p in procs:
+                        p.wait(timeout=10)
+                except subprocess.TimeoutExpired:
+                    stop(signal.SIGKILL)
+                    for p in procs:
+                        p.wait()
+                break
+            time.sleep(0.2)
+    except BaseException:
+        stop(signal.SIGKILL)
+        raise
+    codes = [p.wait() for p in procs]
+    for t in relays:
+        t.join(timeout=5)
+    if any(codes):
+        print(f"bench: rank exit codes {codes}" + (" (deadline reached)" if time.monotonic() > t_end else ""),
+              file=sys.stderr, flush=True)
+        return 1
+    return 0
+
+
+# plain `python bench.py --gpus N` (N > 1) outside torch.distributed.run: become the launcher of the
+# N ranks, before anything below imports torch or libgolhip
+if __name__ == "__main__" and "WORLD_SIZE" not in os.environ and _argv_int(sys.argv[1:], "--gpus", 1) > 1:
+    sys.exit(launch_ranks(sys.argv[1:], _argv_int(sys.argv[1:], "--gpus", 1),
+                          float(_argv_int(sys.argv[1:], "--launch-deadline-s", 1500))))
+
 import torch  # noqa: E402  (first: one HIP runtime per process, see golhip.py)
 import torch.distributed as dist  # noqa: E402
 
@@ -104,7 +209,12 @@ GOLDEN = ROOT / "tests" / "golden"
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one process per GPU). Under torch.distributed.run: must equal "
+                         "WORLD_SIZE; run plainly with N > 1, bench.py starts the N rank processes "
+                         "itself (launch_ranks)")
+    ap.add_argument("--launch-deadline-s", type=int, default=1500,
+                    help="plain --gpus N > 1 runs: the launcher kills every rank after this long")
     ap.add_argument("--steps", type=int, default=1000, help="timed generations (configs[2]: 1000 turns)")
     ap.add_argument("--warmup", type=int, default=8, help="untimed generations")
     ap.add_argument("--size", type=int, default=65536, help="board width")
@@ -666,8 +776,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
-        if world == 1 and a.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
+        if world == 1 and a.gpus > 1:  # bench.main() called in-process; `python bench.py` launches the ranks
+            raise SystemExit("--gpus N > 1: run `python bench.py --gpus N` (it starts the N ranks) or "
+                             "launch it with torch.distributed.run")
     # test hook (tests/test_gpu_rank_host.py): GOLHIP_HOST_COMM=1 runs the rank engines with the gloo
     # host transport instead of RCCL, so N ranks can share the one GPU of a test box (RCCL refuses
     # two ranks on one device); the engine, its launch plan and the timed region are unchanged

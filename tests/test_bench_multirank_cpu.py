@@ -19,11 +19,11 @@ import socket
 import sys
 from pathlib import Path
 
-import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
 from conftest import PKG, ROOT
+from fake_engine import FakeEngine
 
 
 def _free_port():
@@ -32,129 +32,6 @@ def _free_port():
     p = s.getsockname()[1]
     s.close()
     return p
-
-
-class _Info:
-    def __init__(self, rows, y0, width):
-        self.rows, self.y0, self.width = rows, y0, width
-
-
-class FakeEngine:
-    """Host stand-in for golhip.Engine in rank mode (the calls bench.py makes), stepping its strip
-    with the oracle and exchanging k-row halos with its ring neighbours over gloo."""
-
-    log = []
-
-    def __init__(self, width, height, ngpus=1, k=1, *, rank=None, world_size=None, device=0,
-                 nccl_id=None, host_comm=None):
-        import golhip
-
-        assert world_size and world_size > 1 and nccl_id is not None and len(nccl_id) > 0
-        assert host_comm is None
-        self.y0, rows = golhip.strip_bounds(height, world_size, rank)
-        self.width, self.height, self.rows, self.k = width, height, rows, k
-        self.rank, self.world = rank, world_size
-        self.buf = np.zeros((rows + 2 * k, width // 64), dtype=np.uint64)
-        self.info = _Info(rows, self.y0, width)
-        self.last_call = "golhip_create_rank"
-        self.turn = 0
-        self.timed = False
-        self.t_ms = 0.0
-        self.launches = 0
-        self.gens = 0
-        FakeEngine.log.append(("create", width, height, rank, world_size))
-
-    def init_random(self, seed):
-        import oracle
-
-        k = self.k
-        self.buf[k:k + self.rows] = oracle.init_random(self.width, self.height, seed,
-                                                       y0=self.y0, y1=self.y0 + self.rows)
-        self.turn = 0
-        FakeEngine.log.append(("init", seed))
-
-    def set_band_rows(self, n):
-        pass
-
-    def set_fixed_k(self, fixed):
-        pass
-
-    def store_words(self):
-        FakeEngine.log.append(("store_words",))
-        return self.buf[self.k:self.k + self.rows].copy()
-
-    def _block(self, K):
-        import golhip
-        import oracle
-        import torch
-        import torch.distributed as dist
-
-        k, buf = self.k, self.buf
-        sent, recvd, reqs, landing = {}, {}, [], []
-        for kind, peer, row, n in golhip.halo_plan(self.height, self.world, self.rank, K):
-            if kind == "send":
-                tag = sent.get(peer, 0)
-                sent[peer] = tag + 1
-                t = torch.from_numpy(buf[k + row:k + row + n].view(np.int64).copy())
-                reqs.append(dist.isend(t, dst=peer, tag=tag))
-            else:
-                tag = recvd.get(peer, 0)
-                recvd[peer] = tag + 1
-                t = torch.empty((n, buf.shape[1]), dtype=torch.int64)
-                reqs.append(dist.irecv(t, src=peer, tag=tag))
-                landing.append((row, n, t))
-        for r in reqs:
-            r.wait()
-        for row, n, t in landing:
-            buf[k + row:k + row + n] = t.numpy().view(np.uint64)
-        # K generations of the strip with K halo rows each side: the rows past the halos are
-        # garbage that reaches the strip's own rows only after K generations
-        ext = np.ascontiguousarray(buf[k - K:k + self.rows + K])
-        oracle.packed_run_words(ext, K, threads=2)
-        buf[k:k + self.rows] = ext[K:K + self.rows]
-
-    def step(self, turns, counts=False):
-        import time
-
-        assert not counts
-        t0 = time.perf_counter()
-        left = turns
-        while left > 0:
-            K = min(self.k, left)
-            self._block(K)
-            left -= K
-            if self.timed:
-                self.launches += 1
-        if self.timed:
-            self.t_ms += (time.perf_counter() - t0) * 1e3
-            self.gens += turns
-        self.turn += turns
-        FakeEngine.log.append(("step", turns))
-
-    def sync(self):
-        pass
-
-    def timing(self, enable):
-        self.timed = bool(enable)
-
-    def kernel_time(self):
-        return self.t_ms, self.launches, self.gens
-
-    def edge_wait(self):
-        return 0.0, self.launches
-
-    def alive_count(self):
-        import torch
-        import torch.distributed as dist
-
-        own = self.buf[self.k:self.k + self.rows]
-        c = int(np.unpackbits(own.view(np.uint8)).sum())
-        t = torch.tensor([c], dtype=torch.int64)  # collective, like the engine's count all-reduce
-        dist.all_reduce(t)
-        return int(t.item())
-
-    def close(self):
-        FakeEngine.log.append(("close",))
 
 
 def _worker(rank, world, port, out_dir, extra=()):
@@ -234,6 +111,55 @@ def test_bench_rank_path_cpu(tmp_path, world):
         assert r["launches"] >= 1 and r["edge_wait_ms"] >= 0 and r["split_blocks"] >= 1, r
     # the line's value is the max over the ranks' timed regions
     assert abs(line["ms_per_step"] * 20 - max(r["timed_ms"] for r in pr)) < 1e-3 * 20 + 1e-6, (line["ms_per_step"], pr)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_plain_launch_cpu(tmp_path, world):
+    """`python bench.py --gpus N` run plainly, as the driver runs the 1-GPU bench (no
+    torch.distributed.run, WORLD_SIZE unset): bench.py starts the N rank processes itself
+    (launch_ranks, before importing torch) and exits with their status; rank 0's line is the
+    command's one stdout line.  tests/fake_site/sitecustomize.py swaps in the CPU engine stand-in
+    in every process the command starts (gloo halos)."""
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(PYTHONPATH=os.pathsep.join([str(ROOT / "tests" / "fake_site"), env.get("PYTHONPATH", "")]),
+               GOLHIP_TEST_FAKE_ENGINE="1", GOLHIP_TEST_FAKE_LOG_DIR=str(tmp_path), OMP_NUM_THREADS="1")
+    shm_before = set(Path("/dev/shm").glob("golhip_bench_*"))
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(world), "--steps", "20",
+                        "--warmup", "5", "--size", "4096", "--strong-size", "1024", "--strong-steps", "16",
+                        "--preheat-ms", "20"],
+                       cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert f"launched {world} rank processes" in r.stderr
+    out = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(out) == 1, r.stdout
+    line = json.loads(out[0])
+    assert line["n_gpus"] == world and line["config"]["height"] == 4096 * world
+    assert [p["rank"] for p in line["per_rank"]] == list(range(world))
+    assert line["process"]["barrier"] == "shared memory"
+    assert line["parity"] is not None and line["parity"]["ok"] and line["parity"]["digest_ok"] is True, line["parity"]
+    logs = [json.loads((tmp_path / f"rank{rank}.log").read_text()) for rank in range(world)]
+    assert [[e for e in lg if e[0] == "create"][0][3] for lg in logs] == list(range(world))
+    assert set(Path("/dev/shm").glob("golhip_bench_*")) <= shm_before
+
+
+def test_bench_plain_launch_rank_failure(tmp_path):
+    """A rank that fails makes the plain launch fail: the launcher stops the other ranks and exits
+    non-zero (no line is taken for a result)."""
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(PYTHONPATH=os.pathsep.join([str(ROOT / "tests" / "fake_site"), env.get("PYTHONPATH", "")]),
+               GOLHIP_TEST_FAKE_ENGINE="1", GOLHIP_TEST_FAKE_FAIL_RANK="1", OMP_NUM_THREADS="1")
+    t = __import__("time").perf_counter()
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "20", "--warmup", "5",
+                        "--size", "2048", "--preheat-ms", "20", "--k", "8", "--pg-timeout-s", "20"],
+                       cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode != 0
+    assert "rank exit codes" in r.stderr, r.stderr[-3000:]
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert __import__("time").perf_counter() - t < 120
 
 
 def test_bench_rank_path_cpu_process_group_barrier(tmp_path):

@@ -201,6 +201,31 @@ def test_bench_rank_path_real_rccl_shared_gpu(tmp_path):
 
 
 @pytest.mark.timeout(300)
+def test_bench_plain_launch_real_rccl_shared_gpu(tmp_path):
+    """`python bench.py --gpus 2` run PLAINLY, as the driver runs the bench (no torch.distributed.run):
+    bench.py starts its two rank processes itself before touching the GPU (launch_ranks), each a
+    real RCCL rank on this one GPU (GOLHIP_RCCL_SHARED_GPU=1).  One JSON line on stdout, exit 0,
+    and the line's parity and board digest (8192 x 16384, seed 3, oracle goldens) must hold."""
+    env = dict(os.environ, GOLHIP_RCCL_SHARED_GPU="1", PYTHONUNBUFFERED="1")
+    for v in ("GOLHIP_HOST_COMM", "WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(v, None)
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--size", "8192", "--steps", "20",
+           "--warmup", "5", "--no-strong", "--preheat-ms", "20", "--comm-timeout-ms", "60000",
+           "--launch-deadline-s", "240"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    assert "launched 2 rank processes" in p.stderr
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), p.stdout
+    line = json.loads(lines[0])
+    (tmp_path / "bench_plain_world2.json").write_text(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["height"] == 16384
+    assert line["transport"].startswith("rccl, every rank on one GPU"), line["transport"]
+    assert line["parity"]["ok"] and line["parity"]["digest_ok"] is True, line["parity"]
+    assert [x["rank"] for x in line["per_rank"]] == [0, 1]
+
+
+@pytest.mark.timeout(300)
 def test_bench_rank_process_rehearsal_ring_of_one(tmp_path):
     """What one rank of the driver's N > 1 run does, on this GPU: bench.py --pg-always creates the
     torch process group over RCCL and runs its collectives at world 1, and GOLHIP_RING_SELF=1 makes
