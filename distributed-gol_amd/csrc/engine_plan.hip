@@ -300,11 +300,14 @@ RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K, bool counting) 
     // 158 slabs) -> 0.583 us/turn (256 slabs), without counts 0.659 -> 0.543; 12 x 6 0.652, 16 x 5
     // 0.654 (profiles/r05/r05y_rows_per_cu_ab.log).  The rows-per-SIMD model orders all four; 16 x 4
     // is a candidate only in one round (larger boards keep the taller slabs' lower halo share).
-    static constexpr Cand kCount16[] = {{16, 6, 12}, {8, 12, 9}, {12, 8, 12}, {12, 7, 12}, {16, 4, 12}};
-    static constexpr Cand kPlain16[] = {{16, 6, 9}, {12, 8, 9}, {8, 12, 9}, {12, 7, 9}, {16, 4, 9}};
+    // Round 6: 12 x 4 (T = 16, 12 rows per SIMD) under the same one-round rule: 2048^2 with every
+    // count 0.503 against 16 x 4's 0.556 us/turn (profiles/r05/r05zc_t16_slabs_ab.log; without
+    // counts: profiles/r06/).
+    static constexpr Cand kCount16[] = {{16, 6, 12}, {8, 12, 9}, {12, 8, 12}, {12, 7, 12}, {16, 4, 12}, {12, 4, 12}};
+    static constexpr Cand kPlain16[] = {{16, 6, 9}, {12, 8, 9}, {8, 12, 9}, {12, 7, 9}, {16, 4, 9}, {12, 4, 9}};
     static constexpr Cand kOther[] = {{8, 8, 4}};
     const Cand *cands = K == 16 ? (counting ? kCount16 : kPlain16) : kOther;
-    const int ncand = K == 16 ? 5 : 1;
+    const int ncand = K == 16 ? 6 : 1;
     double best = 1e300;
     for (int i = 0; i < ncand; ++i) {
         const Cand c = cands[i];
@@ -313,7 +316,7 @@ RegKernel pick_reg_kernel(golhip_t h, int64_t rows_total, int K, bool counting) 
         if (T < 1) continue;
         const int64_t slabs = (rows_total + T - 1) / T * ((h->wd + kTileChunkWords - 1) / kTileChunkWords);
         const int64_t rounds = (slabs + cus - 1) / cus;
-        if (c.S == 4 && rounds > 1) continue;  // 16 x 4: measured in one round only
+        if (c.S == 4 && rounds > 1) continue;  // 16 x 4, 12 x 4: measured in one round only
         const double cost = (double)rounds * (double)((c.W + 3) / 4) * c.S;
         if (cost < best) {  // ties keep the earlier (measured-preferred) shape
             best = cost;
@@ -327,6 +330,9 @@ bool board_applies(golhip_t h, int *W, int *R) {
     // the production kernel family only, and no forced kernel or band (tests, tuning)
     if (!h->board_kernel || h->split || h->shards.size() != 1 || h->variant != kVariantProd) return false;
     if (h->force_split > 0 || h->force_tile >= 0 || h->force_slab >= 0 || h->band_rows > 0) return false;
+    // golhip_set_fixed_k: every launch exactly k deep (depth sweeps measure the stencil kernels at
+    // that depth; the whole-board kernel is not a k-deep launch)
+    if (h->fixed_k) return false;
     if (h->board_kernel < 0 && h->height > kBoardAutoRows) return false;
     return stencil_board_shape(h->height, h->wd, W, R);
 }

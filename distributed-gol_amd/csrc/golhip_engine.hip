@@ -132,7 +132,7 @@ void free_shard(Shard &s, int64_t drain_ms, bool comm_failed) {
     if (s.pin_counts) (void)hipHostFree(s.pin_counts);
     for (void *q : {(void *)s.diffbuf, (void *)s.ring, (void *)s.ex_rowcounts, (void *)s.ex_offsets,
                     (void *)s.ex_slot_counts, (void *)s.ex_xy, (void *)s.stage, (void *)s.ex_block_sums,
-                    (void *)s.act, (void *)s.act_stats, (void *)s.pflags})
+                    (void *)s.act, (void *)s.act_stats, (void *)s.pflags, (void *)s.psave})
         if (q) (void)hipFree(q);
     if (s.ev_ready) (void)hipEventDestroy(s.ev_ready);
     if (s.ev_halo) (void)hipEventDestroy(s.ev_halo);

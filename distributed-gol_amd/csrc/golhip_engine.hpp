@@ -110,6 +110,7 @@ struct Shard {
     // golhip_step_persistent: one block counter per slab + the error word
     uint32_t *pflags = nullptr;
     int64_t pflags_cap = 0;
+    uint32_t *psave = nullptr;  // the board as of the call's start (restored when a window fails)
 };
 
 struct TimingPair {
@@ -133,7 +134,7 @@ struct GraphEntry {
 
 // Fault injection of the tuning library (GOLHIP_FAULT, tests/test_gpu_failfast.py); none in
 // production.
-enum class Fault { none, stall, skip_send };
+enum class Fault { none, stall, skip_send, slab_stall };
 
 }  // namespace golhip
 
@@ -146,6 +147,7 @@ struct golhip_engine {
     int count_window = 4096;            // generations per count-window finalize
     int variant = golhip::kVariantProd; // fastest measured per depth (golhip_internal.hpp)
     int cus = 0;                        // compute units of the first device (grid sizing)
+    int persistent_limit = 0;           // golhip_set_persistent_limit: slabs the caller owns CUs for (0 = all)
     bool fixed_k = false;               // golhip_set_fixed_k: long runs launch exactly k deep
     bool track_flips = false;  // golhip_track_flips: every step ends with a flips-writing launch
     bool diff_valid = false;   // shards' diffbuf holds the flips of the last generation

@@ -1,20 +1,28 @@
 // stencil_slabq.hip -- gol_slabq, a PERSISTENT gol_slab2 (counting, end flush) that runs a whole
 // count window of K-generation blocks in one launch: golhip_step_persistent, an opt-in call
-// (DESIGN §3 "Round 5").  At configs[1] / configs[4] every slab has its own CU and ~3.3 us of every
-// 16-generation launch is its boundary (ramp, row loads, tail); here a slab waits only for the
-// 3 x 3 neighbourhood of slabs (the ones whose rows its next block reads, and that read its
-// rows) to finish the previous block, instead of for a launch boundary: configs[4]'s board 0.682
-// -> 0.644 us/turn, configs[1]'s 0.755 -> 0.698 (profiles/r05/r05w_persistent_slab.log).
-// Opt-in, not automatic: progress needs every slab resident at once (nothing else on the GPU),
-// and the sc1 hand-off below is MI355X_MICROARCH.md's measured form, not an architectural one.
+// (DESIGN.md "Persistent slab").  At configs[1] / configs[4] every slab has its own CU and ~3.3 us of
+// every 16-generation launch is its boundary (ramp, row loads, tail); here a slab waits only for the
+// 3 x 3 neighbourhood of slabs (the ones whose rows its next block reads, and that read its rows) to
+// finish the previous block, instead of for a launch boundary.
 //
-// Hand-off (MI355X_MICROARCH.md "Valid forms", table row 1): every store of the board is an `sc1`
-// buffer store, every storing wave waits vmcnt(0), a workgroup barrier, then one lane stores the
-// slab's block counter with an `sc1` store; the consumer's wave 0 polls its neighbours' counters
-// with `sc1` loads, a workgroup barrier, then every load of the board is an `sc1` buffer load.  The
-// grid is one workgroup per slab and the host requires slabs <= CUs, so every workgroup is
-// resident; a poll that waits longer than kSpinTicks sets *err and the workgroup leaves (its
-// neighbours then time out too), so the launch always drains.
+// Hand-off, in the memory model's own terms (an agent-scope release / acquire pair per block):
+// every board store is an `sc1` (write-through) buffer store; every storing wave waits vmcnt(0), a
+// workgroup barrier, then lane 0 issues an agent-scope RELEASE fence, waits vmcnt(0) (inline asm:
+// the compiler may drop its own wait after the write-back, /opt/skills/guides/MI355X_MICROARCH.md
+// "Compiler hazard") and stores the slab's block counter (relaxed, agent scope).  The consumer's wave
+// 0 polls its neighbours' counters (relaxed), issues ONE agent-scope ACQUIRE fence, waits vmcnt(0),
+// then a workgroup barrier; board loads are `sc1` buffer loads.  Round 5 ran the `sc1`-only form (no
+// fences: the guide's measured hand-off, not an architectural guarantee); building with
+// -DGOLHIP_SLABQ_SC1_HANDOFF restores it for the A/B (scripts/probe_slabq.py).
+//
+// Residency: the grid is one workgroup per slab (rounded up to a multiple of the 8 XCDs; the
+// surplus workgroups exit at once) and the host refuses the call, before touching the board, unless
+// the occupancy query puts the whole grid on the chip at once and the slabs fit the caller's limit
+// (golhip_set_persistent_limit).  Still, another process or stream can take CUs: a poll that waits
+// longer than kSpinTicks (or sees another slab's failure) sets *err and the workgroup leaves, every
+// later window's workgroups leave at entry, and the host restores the board it saved before the
+// call -- a failed call leaves the board and turn as they were (GOLHIP_ERR_STATE), never half
+// advanced.
 #include "golhip_engine.hpp"
 #include "stencil_tile.hpp"
 
@@ -27,7 +35,7 @@ constexpr uint64_t kSpinTicks = 20000000;   // 200 ms of s_memrealtime (100 MHz)
 template <int K, int W, int S>
 __global__ __launch_bounds__(64 * W) void gol_slabq(uint32_t *buf0, uint32_t *buf1, StencilParams p,
                                                     unsigned long long *slots, uint32_t *flags, int nblocks,
-                                                    uint32_t *err) {
+                                                    uint32_t *err, int stall_group) {
     constexpr int T = W * S - 2 * K;
     static_assert(T >= 1 && K >= 2 && K <= 16 && W >= 2 && S >= 3, "slab geometry");
     __shared__ uint32_t ex[2][W + 2][4][64];
@@ -39,6 +47,8 @@ __global__ __launch_bounds__(64 * W) void gol_slabq(uint32_t *buf0, uint32_t *bu
     const int64_t per_xcd = (ngroups + kXcds - 1) / kXcds;
     const int64_t group = (int64_t)(blockIdx.x % kXcds) * per_xcd + blockIdx.x / kXcds;
     if (group >= ngroups) return;  // whole workgroup; never waited for
+    // an earlier window of this call failed: touch nothing (the host restores the board)
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
     const int nb = (int)p.nbands, nc = (int)p.nchunks;
     const int bi = (int)group / nc, ci = (int)group - bi * nc;
     int ya, yb;
@@ -86,15 +96,25 @@ __global__ __launch_bounds__(64 * W) void gol_slabq(uint32_t *buf0, uint32_t *bu
                 const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
                 uint32_t stop = 0;
                 for (;;) {
+                    // lanes 0..14: the neighbourhood's block counters; lane 15: the error word
                     const uint32_t f = lane < 15 ? __hip_atomic_load(pflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                                 : (uint32_t)blk;
-                    if (__builtin_amdgcn_ballot_w64(f < (uint32_t)blk) == 0) break;
+                                     : lane == 15 ? __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                                  : (uint32_t)blk;
+                    if (__builtin_amdgcn_ballot_w64(lane == 15 && f != 0u) != 0) {
+                        stop = 1;  // another slab failed: nothing this one computes is kept
+                        break;
+                    }
+                    if (__builtin_amdgcn_ballot_w64(lane < 15 && f < (uint32_t)blk) == 0) break;
                     if (__builtin_amdgcn_s_memrealtime() - t0 > kSpinTicks) {
                         stop = 1;
                         break;
                     }
                     __builtin_amdgcn_s_sleep(1);
                 }
+#ifndef GOLHIP_SLABQ_SC1_HANDOFF
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
                 if (lane == 0) {
                     quit = stop;
                     if (stop) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -211,13 +231,18 @@ __global__ __launch_bounds__(64 * W) void gol_slabq(uint32_t *buf0, uint32_t *bu
             for (int g = 1; g < K; ++g) gen(No{}, No{}, Yes{}, g);
             gen(Yes{}, No{}, Yes{}, K);
         }
-        // publish: this workgroup's board stores have drained, then its block counter (sc1); the
-        // count atomics go after it, off the neighbours' critical path (only the finalize after
-        // the launch reads them)
+        // publish: this workgroup's board stores have drained, a release, then its block counter;
+        // the count atomics go after it, off the neighbours' critical path (only the finalize
+        // after the launch reads them)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // also: every generation's per-wave counts are in LDS
-        if (w == 0 && lane == 0)
+        if (w == 0 && lane == 0 && !(group == stall_group && blk == 0)) {  // stall_group: fault injection
+#ifndef GOLHIP_SLABQ_SC1_HANDOFF
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
             __hip_atomic_store(flags + group, (uint32_t)(blk + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         for (int j = w; j < K; j += W) {
             uint32_t acc[1] = {cnt_sum(j)};
             flush_counts<1>(acc, j, lane, group, bslots);
@@ -226,12 +251,27 @@ __global__ __launch_bounds__(64 * W) void gol_slabq(uint32_t *buf0, uint32_t *bu
 }
 
 template <int W, int S>
+const void *slabq_fn() {
+    return reinterpret_cast<const void *>(&gol_slabq<16, W, S>);
+}
+
+// Workgroups of slab shape `shape` (W * 100 + S) the device holds at once (occupancy x CUs).
+int slabq_resident(golhip_t h, int shape, int64_t *out) {
+    const void *fn = shape == 1207 ? slabq_fn<12, 7>() : shape == 1606 ? slabq_fn<16, 6>()
+                   : shape == 1208 ? slabq_fn<12, 8>() : slabq_fn<16, 4>();
+    int per_cu = 0;
+    HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * (shape / 100), 0));
+    *out = (int64_t)per_cu * h->cus;
+    return GOLHIP_OK;
+}
+
+template <int W, int S>
 hipError_t launch_slabq(uint32_t *b0, uint32_t *b1, const StencilParams &q, unsigned long long *slots,
-                        uint32_t *flags, int nblocks, uint32_t *err, hipStream_t s) {
+                        uint32_t *flags, int nblocks, uint32_t *err, int stall_group, hipStream_t s) {
     const int64_t ngroups = q.nbands * (int64_t)q.nchunks;
     const unsigned blocks = (unsigned)((ngroups + kXcds - 1) / kXcds * kXcds);
     hipLaunchKernelGGL((gol_slabq<16, W, S>), dim3(blocks), dim3(64 * W), 0, s, b0, b1, q, slots, flags, nblocks,
-                       err);
+                       err, stall_group);
     return hipGetLastError();
 }
 
@@ -244,6 +284,8 @@ extern "C" {
 
 // golhip_step_persistent (include/golhip.h): golhip_step with per-turn counts through gol_slabq on
 // single-strip boards whose counting launch is a production gol_slab2 shape with one slab per CU.
+// Refuses (GOLHIP_ERR_STATE, nothing enqueued) unless every slab can be resident at once; saves the
+// board first and restores it when a window fails, so a failed call leaves board and turn unchanged.
 int golhip_step_persistent(golhip_t h, int64_t turns, uint64_t *alive_per_turn) {
     if (!h || !alive_per_turn || turns < 0) return GOLHIP_ERR_ARG;
     if (turns == 0) return GOLHIP_OK;
@@ -265,10 +307,20 @@ int golhip_step_persistent(golhip_t h, int64_t turns, uint64_t *alive_per_turn) 
     q.nbands0 = q.nbands = (s.rows + T - 1) / T;
     q.nchunks = (int32_t)((h->wd + kTileChunkWords - 1) / kTileChunkWords);
     const int64_t ngroups = q.nbands * (int64_t)q.nchunks;
+    const int64_t grid = (ngroups + kXcds - 1) / kXcds * kXcds;
     if (ngroups > h->cus || q.wrap_rows <= 0 || q.nbands < 3)
         return fail(h, GOLHIP_ERR_STATE, "golhip_step_persistent: %lld slabs (more than the %d CUs, or under 3 bands)",
                     (long long)ngroups, h->cus);
     HIPCHK(h, hipSetDevice(s.device));
+    // co-residency, before anything is enqueued: the whole grid on the chip at once (occupancy
+    // query), and the slabs within the CUs the caller says it owns (golhip_set_persistent_limit)
+    int64_t resident = 0;
+    if (int rc = slabq_resident(h, shape, &resident)) return rc;
+    if (grid > resident || (h->persistent_limit > 0 && ngroups > h->persistent_limit))
+        return fail(h, GOLHIP_ERR_STATE,
+                    "golhip_step_persistent: %lld slabs (grid %lld) cannot all be resident: the device holds %lld "
+                    "such workgroups at once, the handle's limit is %d (golhip_set_persistent_limit); board unchanged",
+                    (long long)ngroups, (long long)grid, (long long)resident, h->persistent_limit);
     if (s.pflags_cap < ngroups + 1) {
         SYNCCHK(h, s.compute);
         if (s.pflags) HIPCHK(h, hipFree(s.pflags));
@@ -277,6 +329,8 @@ int golhip_step_persistent(golhip_t h, int64_t turns, uint64_t *alive_per_turn) 
         HIPCHK(h, hipMalloc(&s.pflags, sizeof(uint32_t) * (ngroups + 1)));
         s.pflags_cap = ngroups + 1;
     }
+    const size_t board_bytes = sizeof(uint32_t) * (size_t)s.rows * (size_t)h->pitch;
+    if (!s.psave) HIPCHK(h, hipMalloc(&s.psave, board_bytes));  // the board's size is fixed per handle
     if (s.dev_counts_cap < (size_t)turns) {
         SYNCCHK(h, s.compute);
         if (s.dev_counts) HIPCHK(h, hipFree(s.dev_counts));
@@ -286,7 +340,11 @@ int golhip_step_persistent(golhip_t h, int64_t turns, uint64_t *alive_per_turn) 
         s.dev_counts_cap = (size_t)std::max<int64_t>(turns, 128);
     }
     uint32_t *const err = s.pflags + ngroups;
+    const int cur0 = h->cur;
+    const int64_t turn0 = h->turn;
+    HIPCHK(h, hipMemcpyAsync(s.psave, h->row0(s, cur0), board_bytes, hipMemcpyDeviceToDevice, s.compute));
     HIPCHK(h, hipMemsetAsync(err, 0, sizeof(uint32_t), s.compute));
+    const int stall_group = h->fault == Fault::slab_stall ? 0 : -1;  // tuning library's fault injection
     // the 16-generation blocks, one launch per count window; a tail under 16 turns: golhip_step
     const int64_t body = turns / K * K;
     for (int64_t done = 0; done < body;) {
@@ -295,11 +353,18 @@ int golhip_step_persistent(golhip_t h, int64_t turns, uint64_t *alive_per_turn) 
         uint32_t *b0 = h->row0(s, h->cur), *b1 = h->row0(s, h->cur ^ 1);
         const int nblocks = (int)(n / K);
         hipError_t e = hipErrorInvalidValue;
-        if (shape == 1207) e = launch_slabq<12, 7>(b0, b1, q, s.slots, s.pflags, nblocks, err, s.compute);
-        if (shape == 1606) e = launch_slabq<16, 6>(b0, b1, q, s.slots, s.pflags, nblocks, err, s.compute);
-        if (shape == 1208) e = launch_slabq<12, 8>(b0, b1, q, s.slots, s.pflags, nblocks, err, s.compute);
-        if (shape == 1604) e = launch_slabq<16, 4>(b0, b1, q, s.slots, s.pflags, nblocks, err, s.compute);
-        if (e != hipSuccess) return fail(h, GOLHIP_ERR_HIP, "gol_slabq: %s", hipGetErrorString(e));
+        if (shape == 1207) e = launch_slabq<12, 7>(b0, b1, q, s.slots, s.pflags, nblocks, err, stall_group, s.compute);
+        if (shape == 1606) e = launch_slabq<16, 6>(b0, b1, q, s.slots, s.pflags, nblocks, err, stall_group, s.compute);
+        if (shape == 1208) e = launch_slabq<12, 8>(b0, b1, q, s.slots, s.pflags, nblocks, err, stall_group, s.compute);
+        if (shape == 1604) e = launch_slabq<16, 4>(b0, b1, q, s.slots, s.pflags, nblocks, err, stall_group, s.compute);
+        if (e != hipSuccess) {  // undo the windows that did run
+            SYNCCHK(h, s.compute);
+            HIPCHK(h, hipMemcpy(h->row0(s, cur0), s.psave, board_bytes, hipMemcpyDeviceToDevice));
+            h->cur = cur0;
+            h->turn = turn0;
+            return fail(h, GOLHIP_ERR_HIP, "gol_slabq: %s (board restored to turn %lld)", hipGetErrorString(e),
+                        (long long)turn0);
+        }
         HIPCHK(h, launch_count_finalize((int)n, s.slots, s.dev_counts + done, s.compute));
         h->cur ^= (nblocks & 1);
         h->turn += n;
@@ -311,13 +376,26 @@ int golhip_step_persistent(golhip_t h, int64_t turns, uint64_t *alive_per_turn) 
                              s.compute));
     HIPCHK(h, hipMemcpyAsync(&errv, err, sizeof errv, hipMemcpyDeviceToHost, s.compute));
     SYNCCHK(h, s.compute);
-    if (errv)
-        return fail(h, GOLHIP_ERR_HIP, "golhip_step_persistent: a slab waited over 200 ms for its neighbours (is the GPU "
-                                       "shared?); the board is no longer consistent: reload it");
+    if (errv) {  // a slab gave up waiting: put the saved board back, as of before the call
+        HIPCHK(h, hipMemcpyAsync(h->row0(s, cur0), s.psave, board_bytes, hipMemcpyDeviceToDevice, s.compute));
+        SYNCCHK(h, s.compute);
+        h->cur = cur0;
+        h->turn = turn0;
+        return fail(h, GOLHIP_ERR_STATE,
+                    "golhip_step_persistent: a slab waited over 200 ms for its neighbours (the GPU is shared?); the "
+                    "board and turn are restored to turn %lld (use golhip_step)", (long long)turn0);
+    }
     const int64_t rep = h->rep();
     if (rep > 1)
         for (int64_t i = 0; i < body; ++i) alive_per_turn[i] /= (uint64_t)rep;
     if (body < turns) return run_steps(h, turns - body, alive_per_turn + body, false);
+    return GOLHIP_OK;
+}
+
+// golhip_set_persistent_limit (include/golhip.h)
+int golhip_set_persistent_limit(golhip_t h, int max_groups) {
+    if (!h || max_groups < 0) return GOLHIP_ERR_ARG;
+    h->persistent_limit = max_groups;
     return GOLHIP_OK;
 }
 

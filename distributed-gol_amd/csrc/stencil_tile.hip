@@ -17,9 +17,13 @@ namespace golhip {
 // Round 5: the packed slab at depths 2 / 4 / 8 / 12 too, for the tails of narrow-board calls
 // (configs[0]'s 100 turns ended in gol_slab 12 + 8 launches at 11.8 + 8.0 us against ~7 us per
 // packed launch: profiles/r05/r05p_cfg0_timeline.log).
+// Round 6: 12 x 4 (T = 16: 12 rows per SIMD against 16 x 4's 16) with and without counts, for boards
+// whose 12 x 4 slabs fit one round over the CUs (2048^2 with every count 0.556 -> 0.503 us/turn in
+// the tuning build, profiles/r05/r05zc_t16_slabs_ab.log; round 6 A/B: profiles/r06/).
 #define GOLHIP_SLAB_PROD_CONFIGS(X) \
     X(8, 8, 8, 4) X(12, 8, 8, 4) X(16, 8, 12, 9) X(16, 16, 6, 9) X(16, 12, 8, 9) X(16, 12, 7, 9) \
-    X(16, 16, 6, 12) X(16, 12, 7, 12) X(16, 12, 8, 12) X(16, 16, 4, 9) X(16, 16, 4, 12) X(16, 4, 3, 14) X(16, 6, 3, 14) X(16, 8, 3, 14) \
+    X(16, 16, 6, 12) X(16, 12, 7, 12) X(16, 12, 8, 12) X(16, 16, 4, 9) X(16, 16, 4, 12) X(16, 12, 4, 9) X(16, 12, 4, 12) \
+    X(16, 4, 3, 14) X(16, 6, 3, 14) X(16, 8, 3, 14) \
     X(12, 4, 3, 14) X(12, 6, 3, 14) X(12, 8, 3, 14) X(8, 4, 3, 14) X(8, 6, 3, 14) X(8, 8, 3, 14) \
     X(4, 4, 3, 14) X(4, 6, 3, 14) X(4, 8, 3, 14) X(2, 4, 3, 14) X(2, 6, 3, 14) X(2, 8, 3, 14)
 

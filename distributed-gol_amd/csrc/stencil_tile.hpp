@@ -1360,6 +1360,7 @@ constexpr int kSlabP = 14;  // gol_slabp: P = 64 / (wd + 2) row segments packed 
 constexpr bool slab_prod_ws(int K, int W, int S) {
     return (K == 16 && W == 8 && S == 12) || (K == 16 && W == 12 && S == 8) ||
            (K == 16 && W == 12 && S == 7) || (K == 16 && W == 16 && S == 6) || (K == 16 && W == 16 && S == 4) ||
+           (K == 16 && W == 12 && S == 4) ||
            (K == 8 && W == 8 && S == 8) ||
            (K == 12 && W == 8 && S == 8) ||
            ((K == 16 || K == 12 || K == 8 || K == 4 || K == 2) && S == 3 && (W == 4 || W == 6 || W == 8));

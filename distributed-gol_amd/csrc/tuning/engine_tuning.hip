@@ -14,6 +14,8 @@
 //     GOLHIP_FAULT=skip_send  the first send of every halo exchange from exchange number
 //                             GOLHIP_FAULT_FROM (default 1) on is left out of the RCCL group: the
 //                             peer's matching receive never completes (a stuck RCCL transfer)
+//     GOLHIP_FAULT=slab_stall golhip_step_persistent's slab 0 never signals its first block: its
+//                             neighbours time out (a slab that is not resident)
 //   Timestamps: GOLHIP_VARIANT=stamp -- per-wave stamps of the last single-strip launch
 //     (golhip_tuning_stamps / golhip_tuning_stamps_ex; scripts/stamp_launch.py, slab_stamps.py).
 #include <chrono>
@@ -63,6 +65,7 @@ void configure(golhip_t h) {
     if (const char *e = std::getenv("GOLHIP_FAULT")) {
         if (std::strcmp(e, "stall") == 0) h->fault = Fault::stall;
         if (std::strcmp(e, "skip_send") == 0) h->fault = Fault::skip_send;
+        if (std::strcmp(e, "slab_stall") == 0) h->fault = Fault::slab_stall;
     }
 }
 

@@ -28,6 +28,7 @@ LIB_PATH = Path(os.environ.get("GOLHIP_LIB", HERE / "lib" / "libgolhip.so"))
 # production kernels plus the measured-and-rejected variants, the level-split / register-tile
 # kernels and the A/B environment selectors.  Only tests of those kernels and tuning scripts load it.
 TUNING_LIB_PATH = HERE / "lib_tuning" / "libgolhip.so"
+FAULTS_LIB_PATH = HERE / "lib_faults" / "libgolhip.so"
 
 OK = 0
 ERR_ARG, ERR_HIP, ERR_OOM, ERR_CAP, ERR_RCCL, ERR_NODEV, ERR_STATE = -1, -2, -3, -4, -5, -6, -7
@@ -40,7 +41,7 @@ EXPORTS = [
     "golhip_halo_plan",
     "golhip_create", "golhip_create_strips", "golhip_nccl_unique_id", "golhip_create_rank",
     "golhip_comm_abort", "golhip_edge_wait", "golhip_set_activity", "golhip_activity_stats",
-    "golhip_set_board_kernel", "golhip_step_persistent",
+    "golhip_set_board_kernel", "golhip_step_persistent", "golhip_set_persistent_limit",
     "golhip_create_rank_host", "golhip_destroy",
     "golhip_last_error", "golhip_get_info", "golhip_load_bytes", "golhip_init_random",
     "golhip_store_bytes", "golhip_store_words", "golhip_load_words", "golhip_step",
@@ -178,6 +179,7 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
         "golhip_load_words": ([H, ctypes.c_void_p], i32),
         "golhip_step": ([H, i64, ctypes.c_void_p], i32),
         "golhip_step_persistent": ([H, i64, ctypes.c_void_p], i32),
+        "golhip_set_persistent_limit": ([H, i32], i32),
         "golhip_alive_count": ([H, u64p], i32),
         "golhip_alive_cells": ([H, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)], i32),
         "golhip_flips": ([H, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)], i32),
@@ -231,8 +233,16 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
 
 def tuning_library() -> ctypes.CDLL:
     """The tuning build (lib_tuning/libgolhip.so): pass it as Engine(..., lib=tuning_library()) to
-    run a non-production kernel (GOLHIP_VARIANT / GOLHIP_SPLIT / GOLHIP_TILE / GOLHIP_SLAB ...)."""
+    run a non-production kernel (GOLHIP_VARIANT / GOLHIP_SPLIT / GOLHIP_TILE / GOLHIP_SLAB ...).
+    Built here; pushed to a GPU box only for the runs that load it (.gpurunignore)."""
     return load_library(TUNING_LIB_PATH)
+
+
+def fault_library() -> ctypes.CDLL:
+    """The production kernels + the tuning library's engine hooks (lib_faults/libgolhip.so): fault
+    injection (GOLHIP_FAULT) and the A/B selectors over the production kernels -- what the fail-fast
+    tests load."""
+    return load_library(FAULTS_LIB_PATH)
 
 
 _default_comm_timeout_ms: int | None = None
@@ -468,10 +478,15 @@ class Engine:
 
     def step_persistent(self, turns: int) -> np.ndarray:
         """golhip_step_persistent: `turns` turns with every count, one persistent-slab launch per
-        count window (opt-in; configs[1] / configs[4]-like boards, nothing else on the GPU)."""
+        count window (opt-in; configs[1] / configs[4]-like boards).  Refuses (GOLHIP_ERR_STATE,
+        board unchanged) when the slabs cannot all be resident; restores the board on a timeout."""
         out = np.zeros(max(turns, 1), dtype=np.uint64)
         self._check(self._L.golhip_step_persistent(self._h, turns, out.ctypes.data))
         return out[:turns]
+
+    def set_persistent_limit(self, max_groups: int) -> None:
+        """golhip_set_persistent_limit: slabs the caller owns CUs for (0 = the whole device)."""
+        self._check(self._L.golhip_set_persistent_limit(self._h, max_groups))
 
     def alive_count(self) -> int:
         v = ctypes.c_uint64()

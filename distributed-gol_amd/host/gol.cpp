@@ -13,6 +13,10 @@
 //                                                                             from the stencil
 //   manageKeyPresses s/q/p/k                                    :105-151   -> serviced between
 //                                                                             chunks
+//   the unbuffered channels that make the turn loop wait for   gol/gol.go:48-54 -> a delivery
+//   every consumer each turn                                                   thread: chunk n's
+//                                                                             events go out while
+//                                                                             chunk n+1 runs
 //   FinalTurnComplete, out/WxHxT.pgm, StateChange Quitting      :235-262   -> same
 //
 // Deliberate deviations from reference quirks, documented in
@@ -23,6 +27,8 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <exception>
 #include <cstdio>
 #include <map>
 #include <mutex>
@@ -104,11 +110,17 @@ std::vector<Cell> to_cells(const std::vector<int32_t> &xy) {
     return out;
 }
 
+int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 struct Ticker {  // gol/distributor.go:168-191 with the 2 s time.Ticker of :228
     std::mutex mu;
+    std::condition_variable cv;
     int64_t turn = 0;
     int64_t count = 0;
-    std::atomic<bool> stop{false};
+    bool stop = false;
     std::thread th;
 
     ~Ticker() { halt(); }  // an exception unwinding Run must not destroy a joinable thread
@@ -116,33 +128,150 @@ struct Ticker {  // gol/distributor.go:168-191 with the 2 s time.Ticker of :228
     void start(Channel<Event> *events, int period_ms) {
         th = std::thread([this, events, period_ms] {
             auto next = std::chrono::steady_clock::now() + std::chrono::milliseconds(period_ms);
-            while (!stop.load()) {
-                std::this_thread::sleep_for(std::chrono::milliseconds(5));
-                if (std::chrono::steady_clock::now() < next) continue;
+            std::unique_lock<std::mutex> lk(mu);
+            for (;;) {
+                // sleep to the tick itself (no polling granularity in the tick latency)
+                if (cv.wait_until(lk, next, [&] { return stop; })) return;
+                const int64_t fired = now_ns();
                 next += std::chrono::milliseconds(period_ms);
-                int64_t t, c;
-                {
-                    std::lock_guard<std::mutex> lk(mu);
-                    t = turn;
-                    c = count;
-                }
+                Event e = Event::alive_cells_count(turn, count);
+                e.FiredNs = fired;
+                lk.unlock();
                 try {
-                    events->send(Event::alive_cells_count(t, c));
+                    events->send(std::move(e));
                 } catch (...) {
                     return;  // events closed
                 }
+                lk.lock();
             }
         });
     }
+    // the latch of gol/distributor.go:180-184: the last turn DELIVERED and its count
     void update(int64_t t, int64_t c) {
         std::lock_guard<std::mutex> lk(mu);
         turn = t;
         count = c;
     }
     void halt() {
-        stop = true;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv.notify_all();
         if (th.joinable()) th.join();
     }
+};
+
+// The ordered event stream of one Run: the turn loop hands each stepped chunk's results (and every
+// other event, in order) to a delivery thread, which turns them into CellFlipped / TurnComplete
+// events on `events` and latches the ticker, while the turn loop already steps the next chunk on the
+// GPU -- device work of chunk n+1 overlaps the delivery of chunk n.  At most `depth` batches wait,
+// so the turn loop runs at most that far ahead of what the consumer has seen (key latency).
+class Pipeline {
+public:
+    struct Batch {
+        int64_t turn0 = 0;                 // turns: completed turns before the chunk
+        std::vector<uint64_t> alive;       // alive after each of the chunk's turns
+        std::vector<uint64_t> per_turn;    // per-turn CellFlipped counts (flip events only)
+        std::vector<int32_t> xy;           // every turn's flipped cells, turn by turn
+        std::vector<Event> events;         // or: these events, as they are
+        bool flips = false;
+    };
+
+    // depth 0: no delivery thread -- each batch is delivered by the turn loop itself before it
+    // steps on (the unpipelined A/B: device work and event delivery alternate)
+    Pipeline(Channel<Event> *events, Ticker *ticker, size_t depth)
+        : events_(events), ticker_(ticker), q_(std::max<size_t>(depth, 1)), inline_(depth == 0) {
+        if (!inline_) th_ = std::thread([this] { deliver(); });
+    }
+    ~Pipeline() {
+        if (th_.joinable()) {  // unwinding: the consumer may not drain events any more
+            q_.close();
+            events_->close();
+            th_.join();
+        }
+    }
+    void turns(int64_t turn0, std::vector<uint64_t> &&alive) {
+        Batch b;
+        b.turn0 = turn0;
+        b.alive = std::move(alive);
+        push(std::move(b));
+    }
+    void flips(int64_t turn0, std::vector<uint64_t> &&alive, std::vector<uint64_t> &&per_turn,
+               std::vector<int32_t> &&xy) {
+        Batch b;
+        b.turn0 = turn0;
+        b.alive = std::move(alive);
+        b.per_turn = std::move(per_turn);
+        b.xy = std::move(xy);
+        b.flips = true;
+        push(std::move(b));
+    }
+    void event(Event e) {
+        Batch b;
+        b.events.push_back(std::move(e));
+        push(std::move(b));
+    }
+    // every batch handed over so far has been delivered
+    void finish() {
+        q_.close();
+        if (th_.joinable()) th_.join();
+        if (failed_) std::rethrow_exception(failed_);
+    }
+
+private:
+    void push(Batch &&b) {
+        if (inline_) {
+            deliver_batch(b);
+            return;
+        }
+        try {
+            q_.send(std::move(b));
+        } catch (...) {  // closed by a failed delivery (failed_ was set before the close)
+            if (failed_) std::rethrow_exception(failed_);
+            throw;
+        }
+    }
+    void deliver_batch(Batch &b) {
+        if (!b.events.empty()) {
+            events_->send_all(std::move(b.events));
+            return;
+        }
+        std::vector<Event> out;
+        size_t at = 0;
+        // the ticker latches a turn once its TurnComplete is on its way (the reference latches on
+        // turnChan, gol/distributor.go:180-184): deliver in slices so a tick never waits for a
+        // whole chunk, and never reports a turn not yet delivered
+        constexpr size_t kSlice = 4096;
+        out.reserve(kSlice + 64);
+        for (size_t i = 0; i < b.alive.size(); ++i) {
+            const int64_t t = b.turn0 + (int64_t)i;  // the turn being computed
+            if (b.flips)  // per turn: CellFlipped{turn} for each flipped cell, then TurnComplete
+                for (uint64_t c = 0; c < b.per_turn[i]; ++c, ++at)
+                    out.push_back(Event::cell_flipped(t, Cell{b.xy[2 * at], b.xy[2 * at + 1]}));
+            out.push_back(Event::turn_complete(t + 1));
+            if (out.size() >= kSlice || i + 1 == b.alive.size()) {
+                events_->send_all(std::move(out));
+                out.clear();
+                ticker_->update(t + 1, (int64_t)b.alive[i]);
+            }
+        }
+    }
+    void deliver() {
+        try {
+            while (auto b = q_.recv()) deliver_batch(*b);
+        } catch (...) {
+            failed_ = std::current_exception();
+            q_.close();
+        }
+    }
+
+    Channel<Event> *events_;
+    Ticker *ticker_;
+    Channel<Batch> q_;
+    bool inline_;
+    std::thread th_;
+    std::exception_ptr failed_;
 };
 
 std::string board_name(const Params &p) {
@@ -223,30 +352,32 @@ void run_impl(const Params &p, Channel<Event> *events, Channel<char> *keyPresses
     Ticker ticker;
     ticker.update(turn, turn == 0 ? (int64_t)initial.size() : (int64_t)eng->alive_count());
     ticker.start(events, o.ticker_ms);
+    Pipeline pipe(events, &ticker, (size_t)std::max(1, o.pipeline_depth));
 
     bool quit = false;
-    // Keys (gol/distributor.go:115-148), serviced between step chunks.
+    // Keys (gol/distributor.go:115-148), serviced between step chunks; their events go through the
+    // pipeline, after every event of the turns before them
     auto handle_key = [&](char key, bool &paused) {
         switch (key) {
             case 's': {
                 const std::string f = name + "x" + std::to_string(turn);
                 snapshot(*eng, p, o, f);
-                events->send(Event::image_output_complete(turn, f));
+                pipe.event(Event::image_output_complete(turn, f));
                 break;
             }
             case 'q': {
                 // Pause{P: true, Turn, Dimension} parks the state in the broker (:139-147): the
                 // checkpoint file outlives this process; a later Run resumes from it
                 eng->checkpoint_save(ckpt);
-                events->send(Event::state_change(turn, State::Quitting));
+                pipe.event(Event::state_change(turn, State::Quitting));
                 quit = true;
                 break;
             }
             case 'k': {
                 const std::string f = name + "x" + std::to_string(turn);
                 snapshot(*eng, p, o, f);
-                events->send(Event::image_output_complete(turn, f));
-                events->send(Event::state_change(turn, State::Quitting));
+                pipe.event(Event::image_output_complete(turn, f));
+                pipe.event(Event::state_change(turn, State::Quitting));
                 eng.reset();  // Broker.Quit -> GolOP.Quit: the workers go away
                 reset_saved_state(o);
                 quit = true;
@@ -254,18 +385,18 @@ void run_impl(const Params &p, Channel<Event> *events, Channel<char> *keyPresses
             }
             case 'p':
                 paused = !paused;
-                events->send(Event::state_change(turn, paused ? State::Paused : State::Executing));
+                pipe.event(Event::state_change(turn, paused ? State::Paused : State::Executing));
                 break;
             default: break;
         }
     };
 
-    // Per-turn CellFlipped: chunks of turns through golhip_step_flips (each turn's flips kept in
-    // a device ring, one extraction per chunk); chunk sizes grow while a chunk takes less than
-    // chunk_seconds, so keys still wait at most about that long.
+    // Chunks of turns: golhip_step with per-turn counts, or golhip_step_flips for per-turn
+    // CellFlipped (each turn's flips kept in a device ring, one extraction per chunk).  Chunk sizes
+    // grow while a chunk's device call takes less than chunk_seconds, so keys wait at most about
+    // that long (plus the pipeline's queued chunks); the events of a chunk are delivered by the
+    // pipeline while the next chunk runs.
     const int64_t ring_cap = o.flip_events ? eng->flips_ring_capacity() : 1;
-    std::vector<int32_t> fxy;
-    std::vector<uint64_t> fper, falive;
     int64_t chunk = 1;
     bool paused = false;
     while (!quit && turn < p.Turns) {
@@ -280,33 +411,24 @@ void run_impl(const Params &p, Channel<Event> *events, Channel<char> *keyPresses
         if (quit) break;
         const auto t0 = std::chrono::steady_clock::now();
         if (o.flip_events) {
-            // per turn: CellFlipped{turn} for each flipped cell, then TurnComplete{turn+1}
             const int64_t n = std::min<int64_t>({chunk, p.Turns - turn, ring_cap});
+            std::vector<int32_t> fxy;
+            std::vector<uint64_t> fper, falive;
             eng->step_flips(n, fxy, fper, falive);
-            size_t at = 0;
-            for (int64_t i = 0; i < n; ++i) {
-                for (uint64_t c = 0; c < fper[(size_t)i]; ++c, ++at)
-                    events->send(Event::cell_flipped(turn, Cell{fxy[2 * at], fxy[2 * at + 1]}));
-                ++turn;
-                ticker.update(turn, (int64_t)falive[(size_t)i]);
-                events->send(Event::turn_complete(turn));
-            }
+            pipe.flips(turn, std::move(falive), std::move(fper), std::move(fxy));
+            turn += n;
         } else {
             const int64_t n = std::min<int64_t>(chunk, p.Turns - turn);
-            const std::vector<uint64_t> c = eng->step(n, true);
-            for (int64_t i = 0; i < n; ++i) {
-                ticker.update(turn + i + 1, (int64_t)c[(size_t)i]);
-                events->send(Event::turn_complete(turn + i + 1));
-            }
+            pipe.turns(turn, eng->step(n, true));
             turn += n;
         }
-        // chunk sized on device time + event delivery, so keys wait at most ~chunk_seconds
         const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         if (dt < o.chunk_seconds && chunk < (1 << 20)) chunk *= 2;
         if (dt > 4 * o.chunk_seconds && chunk > 1) chunk /= 2;
     }
 
     if (quit) {  // 'q' / 'k': FinalTurnComplete with no cells (gol/distributor.go:128,147)
+        pipe.finish();
         ticker.halt();
         events->send(Event::final_turn_complete(turn, {}));
         events->close();
@@ -314,6 +436,7 @@ void run_impl(const Params &p, Channel<Event> *events, Channel<char> *keyPresses
     }
 
     std::vector<Cell> alive = to_cells(eng->alive_cells());  // gol/distributor.go:235
+    pipe.finish();
     ticker.halt();
     events->send(Event::final_turn_complete(turn, std::move(alive)));
     snapshot(*eng, p, o, name + "x" + std::to_string(p.Turns));  // out/WxHxT.pgm (:246-253)

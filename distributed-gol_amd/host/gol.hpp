@@ -60,6 +60,9 @@ struct Event {
     State NewState = State::Executing;
     Cell cell;
     std::shared_ptr<std::vector<Cell>> Alive;  // FinalTurnComplete only
+    // AliveCellsCount only, a host-mirror extra (no gol/event.go field): steady_clock ns at which
+    // the ticker fired, so a consumer can measure tick latency (fire -> received)
+    int64_t FiredNs = 0;
 
     // gol/event.go:71-131: the GUI prints events whose String() is non-empty (sdl/loop.go:44-47)
     std::string String() const;
@@ -94,6 +97,9 @@ struct RunOptions {
     bool flip_events = true;           // per-turn CellFlipped (gol/distributor.go:53-59)
     int ticker_ms = 2000;              // AliveCellsCount period (gol/distributor.go:228)
     double chunk_seconds = 0.02;       // target device time per step chunk (key/ticker latency)
+    // stepped chunks whose events may wait for delivery by the delivery thread while the turn
+    // loop steps on (0: no delivery thread, device work and event delivery alternate)
+    int pipeline_depth = 2;
     // The broker's paused state (worldSave, turn, size; broker/broker.go:124-155) as a file: 'q'
     // writes it, the next Run with Turns > 0 consumes it (CheckStates) and resumes when the size
     // matches.  Empty: <out_dir>/broker_state.ckpt.

@@ -87,7 +87,8 @@ int golhip_halo_plan(int64_t height, int world_size, int rank, int k, golhip_xfe
 /* ---- lifetime --------------------------------------------------------------------------- */
 /* One process, `ngpus` devices (0..ngpus-1), one row strip each
  * (the on-node replacement of the broker + 4 servers, broker/broker.go:191-205), halos moved by
- * peer copies over xGMI. k = max generations per stencil launch (1..32). */
+ * peer copies over xGMI. k = max generations per temporal-blocking stencil launch (1..32; the
+ * whole-board kernel of golhip_set_board_kernel is not bounded by it). */
 int golhip_create(int width, int height, int ngpus, int k, golhip_t *out);
 /* One process, `nstrips` row strips placed on devices 0..ndevices-1 (strip s on device
  * s*ndevices/nstrips), halos by peer copies.  golhip_create(w, h, n, k) == create_strips(w, h, n, n, k);
@@ -259,21 +260,31 @@ int golhip_sync(golhip_t h);                         /* wait for all queued devi
  * to 512 whose lcm with 128 is one of them: the reference's 16/64/128/256/512 sizes) and 4 W R rows
  * (4 ... 512) runs in ONE workgroup holding the whole torus in registers, every golhip_step call as
  * one launch per 4096 generations: no temporal-blocking trapezoid, no halo lanes, no launch
- * boundary inside a call.  enable = -1 (default): boards of at most 256 rows (one CU does the
+ * boundary inside a call.  Its launches are therefore NOT bounded by the handle's k (the depth of
+ * the temporal-blocking stencil launches; golhip_launch_plan lists them as up to 4096 deep), and
+ * golhip_set_fixed_k(h, 1) turns it off (a depth sweep measures the k-deep stencil launches).  enable = -1 (default): boards of at most 256 rows (one CU does the
  * board's whole VALU work per generation: faster than the multi-workgroup slabs up to 256 rows,
  * slower at 512), 1: every board it fits, 0: never (A/B).  golhip_launch_kind reports it as
  * kind 4 (*param = 100 * waves + rows per segment).  GOLHIP_ERR_ARG outside -1 .. 1. */
 int golhip_set_board_kernel(golhip_t h, int enable);
 /* golhip_step with per-turn counts (alive_per_turn non-null) as ONE launch per count window of a
  * persistent slab kernel (gol_slabq): each slab waits for its 3 x 3 neighbourhood of slabs
- * through device counters instead of for a launch boundary every 16 generations; the same board
- * and counts as golhip_step (a tail under 16 turns runs through it).  Opt-in, for single-strip
- * boards whose counting launch is a gol_slab2 12x7 / 16x6 / 12x8 / 16x4 slab with at most one slab per
- * CU (configs[1], configs[4]; GOLHIP_ERR_STATE otherwise), a handle with k >= 16 and flip
- * tracking off (golhip_track_flips: GOLHIP_ERR_STATE, use golhip_step): its progress
- * needs every slab resident at once, so nothing else may occupy the GPU; a slab that waits over
- * 200 ms fails the call with GOLHIP_ERR_HIP and leaves the board inconsistent (reload it). */
+ * through device counters (agent-scope release / acquire) instead of for a launch boundary every 16
+ * generations; the same board and counts as golhip_step (a tail under 16 turns runs through it).
+ * Opt-in, for single-strip boards whose counting launch is a gol_slab2 12x7 / 16x6 / 12x8 / 16x4 slab
+ * with at most one slab per CU (configs[1], configs[4]; GOLHIP_ERR_STATE otherwise), a handle with
+ * k >= 16 and flip tracking off (golhip_track_flips: GOLHIP_ERR_STATE, use golhip_step).  Its
+ * progress needs every slab resident at once: the call refuses with GOLHIP_ERR_STATE, before any
+ * device work, when the occupancy query does not put the whole grid on the device or the slabs
+ * exceed golhip_set_persistent_limit.  If a slab still waits over 200 ms (another process took
+ * CUs) the call restores the board and turn it started from and returns GOLHIP_ERR_STATE: a failed
+ * call never leaves the board half advanced (the reference's Publish gate never leaves the world
+ * half-written either, broker/broker.go:109-120). */
 int golhip_step_persistent(golhip_t h, int64_t turns, uint64_t *alive_per_turn);
+/* The CUs the caller owns for golhip_step_persistent: at most max_groups slabs (one workgroup per
+ * CU each) may be assumed resident at once -- for a process sharing the GPU with other work (a
+ * second engine, a CU-masked stream, another process).  0 (default): the whole device. */
+int golhip_set_persistent_limit(golhip_t h, int max_groups);
 /* Stable-slab skipping: the register-slab launches of single-strip boards skip every slab whose
  * neighbourhood did not change in the previous launch's last generation -- Life's radius-1 rule
  * keeps such a slab fixed for the launch's K generations -- copying it once and counting its cached

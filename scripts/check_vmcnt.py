@@ -42,15 +42,19 @@ VMEM = re.compile(r"^(buffer_|global_|scratch_|flat_)")
 
 
 def device_object(obj: Path, tmp: Path) -> Path:
-    """Extract the gfx950 code object of a HIP object file (llvm-objdump --offloading)."""
-    local = tmp / obj.name
-    shutil.copy(obj, local)
-    subprocess.run([str(LLVM / "llvm-objdump"), "--offloading", str(local)], cwd=tmp,
+    """Extract the gfx950 code object of a HIP object file: its .hip_fatbin section, unbundled by
+    clang-offload-bundler (which also inflates the compressed bundles --offload-compress writes;
+    llvm-objdump --offloading hands those out still compressed)."""
+    fat = tmp / (obj.name + ".fatbin")
+    subprocess.run([str(LLVM / "llvm-objcopy"), "--dump-section", f".hip_fatbin={fat}", str(obj), os.devnull],
                    check=True, capture_output=True)
-    found = sorted(tmp.glob(obj.name + ".*gfx950*"))
-    if not found:
-        raise SystemExit(f"{obj}: no gfx950 code object")
-    return found[0]
+    co = tmp / (obj.name + ".gfx950.co")
+    r = subprocess.run([str(LLVM / "clang-offload-bundler"), "--type=o", "--unbundle",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fat}", f"--output={co}"],
+                       capture_output=True, text=True)
+    if r.returncode != 0 or not co.exists() or co.stat().st_size == 0:
+        raise SystemExit(f"{obj}: no gfx950 code object ({r.stderr.strip()})")
+    return co
 
 
 def kernel_metadata(co: Path) -> dict[str, dict[str, int]]:

@@ -5,6 +5,7 @@
 #include <fstream>
 #include <string>
 #include <thread>
+#include <vector>
 
 #include "../../distributed-gol_amd/host/gol.hpp"
 
@@ -52,6 +53,27 @@ int main(int argc, char **argv) {
         for (int i = 0; i < 4; ++i) EXPECT(ch.recv().value_or(-1) == i, "fifo order");
         EXPECT(!ch.recv(), "drained");
         EXPECT(!ch.try_recv(), "try_recv on empty");
+    }
+    // send_all: one batch through a small buffer, received in order by a slower consumer
+    // (the delivery thread's TurnComplete slices, host/gol.cpp Pipeline); unbuffered: rendezvous each
+    for (size_t cap : {size_t(0), size_t(3), size_t(1000)}) {
+        Channel<int> ch(cap);
+        std::vector<int> got;
+        std::thread t([&] {
+            while (auto v = ch.recv()) got.push_back(*v);
+        });
+        std::vector<int> batch;
+        for (int i = 0; i < 5000; ++i) batch.push_back(i);
+        ch.send_all(std::move(batch));
+        ch.send_all({5000, 5001});
+        ch.close();
+        t.join();
+        bool ordered = got.size() == 5002;
+        for (size_t i = 0; ordered && i < got.size(); ++i) ordered = got[i] == (int)i;
+        EXPECT(ordered, "send_all lost or reordered elements");
+        bool threw = false;
+        try { ch.send_all({1}); } catch (...) { threw = true; }
+        EXPECT(threw, "send_all on closed channel must fail");
     }
     // PGM round trip, byte-exact with the reference's files (header "P5\n<W> <H>\n255\n")
     for (const char *n : {"16x16", "64x64", "512x512"}) {

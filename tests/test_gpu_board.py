@@ -106,3 +106,19 @@ def test_board_launch_plan(golhip):
     assert golhip.launch_plan(64, 64, 16, 10000) == [4096, 4096, 1808]
     assert golhip.launch_plan(512, 512, 16, 100) != [100]  # 512 rows: the slab kernels (automatic)
     assert golhip.launch_plan(512, 512, 16, 100, strips=2) != [100]  # strips: not the board kernel
+
+
+def test_fixed_k_turns_the_board_kernel_off(golhip, oracle):
+    """golhip_set_fixed_k: every launch exactly k deep, so a depth sweep measures the k-deep stencil
+    launches, not the whole-board kernel (which is not bounded by k); same results either way."""
+    words = oracle.init_random(256, 128, seed=3)
+    with golhip.Engine(256, 128, k=8) as e:
+        assert e.launch_kind(8)[0] == "board"
+        e.set_fixed_k(True)
+        assert e.launch_kind(8)[0] != "board", e.launch_kind(8)
+        e.load_words(words)
+        c = e.step(40, counts=True)
+        got = e.store_words()
+    ref = words.copy()
+    exp = oracle.packed_run_words(ref, 40)
+    assert np.array_equal(c.astype(np.int64), exp) and np.array_equal(got, ref)

@@ -4,9 +4,9 @@ instead of hanging the run (the reference has no such bound: a dead server stall
 Broker.Publish forever, broker/broker.go:58-84).
 
 Each case runs in FRESH processes under their own time limits, so a failure of the deadline itself
-ends in a killed child, not a hung test session.  Fault injection is in the tuning library only
-(csrc/tuning/engine_tuning.hip, GOLHIP_FAULT); the engine code under test is the production code
-both libraries share.
+ends in a killed child, not a hung test session.  Fault injection is in the tuning library's engine
+hooks only (csrc/tuning/engine_tuning.hip, GOLHIP_FAULT), loaded here from lib_faults (the
+production objects + those hooks); the engine code under test is the production code.
   * stuck receive: TWO real RCCL ranks on this one GPU (a distinct NCCL_HOSTID per rank makes RCCL
     build a 2-rank communicator over its network transport instead of refusing "Duplicate GPU");
     rank 1 leaves the first send of every halo exchange out of its RCCL group (GOLHIP_FAULT=
@@ -45,7 +45,7 @@ try:
     if case == "stall":
         # created under the default deadline (a first RCCL set-up in a fresh process can take
         # seconds), then the handle's own deadline
-        e = golhip.Engine(640, 64, k=4, rank=0, world_size=1, device=0, lib=golhip.tuning_library())
+        e = golhip.Engine(640, 64, k=4, rank=0, world_size=1, device=0, lib=golhip.fault_library())
         e.set_comm_timeout(timeout_ms)
         out["halo_rows"] = e.info.halo_rows
         e.init_random(5)
@@ -90,7 +90,7 @@ faulthandler.dump_traceback_later(75, exit=False)  # the Python stack of a child
 import torch  # one HIP runtime per process (golhip.py)
 import golhip
 out = {"rank": rank}
-L = golhip.tuning_library()
+L = golhip.fault_library()
 if rank == 0:
     nid = golhip.nccl_unique_id()  # rank 0 hosts the bootstrap root
     with open(idfile + ".tmp", "wb") as f:
@@ -250,3 +250,84 @@ def test_ring_of_one_still_exchanges_with_a_deadline(golhip, oracle, monkeypatch
     ref_counts = oracle.packed_run_words(ref, 3 * k + 5)
     assert (got == ref).all()
     assert (counts.astype("int64") == ref_counts).all()
+
+
+CHILD_SLAB = r"""
+import hashlib, json, os, sys, time
+sys.path.insert(0, sys.argv[1])
+import torch  # one HIP runtime per process (golhip.py)
+import numpy as np
+import golhip
+out = {}
+with golhip.Engine(4096, 4096, k=16, lib=golhip.fault_library()) as e:  # GOLHIP_FAULT=slab_stall
+    e.init_random(11)
+    e.step(32)
+    before = hashlib.sha256(e.store_words().tobytes()).hexdigest()
+    t0 = time.perf_counter()
+    try:
+        e.step_persistent(600)
+        out["raised"] = False
+    except golhip.GolHipError as err:
+        out["raised"], out["code"], out["msg"] = True, err.code, str(err)
+    out["seconds"] = time.perf_counter() - t0
+    out["turn"] = e.turn
+    out["board_unchanged"] = hashlib.sha256(e.store_words().tobytes()).hexdigest() == before
+    # the handle keeps working: golhip_step from the restored board
+    c = e.step(48, counts=True)
+    out["after_counts"] = [int(x) for x in c[-3:]]
+    out["after_turn"] = e.turn
+    out["after_digest"] = hashlib.sha256(e.store_words().tobytes()).hexdigest()
+with golhip.Engine(4096, 4096, k=16) as e:  # the production library, same board, no fault
+    e.init_random(11)
+    e.step(32 + 48)
+    out["ref_digest"] = hashlib.sha256(e.store_words().tobytes()).hexdigest()
+print(json.dumps(out), flush=True)
+"""
+
+
+def test_persistent_slab_timeout_restores_board():
+    """golhip_step_persistent when a slab never signals (GOLHIP_FAULT=slab_stall, tuning library:
+    slab 0 skips its first block counter, as a slab that is not resident would): its neighbours give
+    up after 200 ms, every later window leaves at entry, and the call returns GOLHIP_ERR_STATE with
+    the board and turn restored to where the call started -- never a half-advanced board (the
+    reference's Publish gate never leaves the world half-written, broker/broker.go:109-120).  The
+    handle keeps working: golhip_step from the restored board ends where an untouched run does."""
+    env = dict(os.environ, GOLHIP_FAULT="slab_stall")
+    p = subprocess.run(["timeout", "-k", "10", "120", sys.executable, "-c", CHILD_SLAB, str(PKG)],
+                       env=env, capture_output=True, text=True, timeout=150)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out["raised"] and out["code"] == -7, out
+    assert "restored to turn 32" in out["msg"], out
+    assert out["turn"] == 32 and out["board_unchanged"], out
+    assert out["seconds"] < 30, out
+    assert out["after_turn"] == 80 and out["after_digest"] == out["ref_digest"], out
+
+
+def test_fault_library_selectors_smoke(golhip, oracle, monkeypatch):
+    """The round-end suite's tuning smoke: the engine hooks (csrc/tuning/engine_tuning.hip) over the
+    production kernels, from lib_faults -- GOLHIP_SLAB forces another production slab shape and
+    GOLHIP_FIXED_K the launch depth, read at create -- bit-exact against the oracle and against the
+    production library's automatic choice."""
+    import numpy as np
+
+    words = oracle.init_random(2048, 2048, seed=13)
+    L = golhip.fault_library()
+    monkeypatch.setenv("GOLHIP_SLAB", "91207")  # gol_slab2 12 x 7 (NC 9)
+    monkeypatch.setenv("GOLHIP_FIXED_K", "1")
+    with golhip.Engine(2048, 2048, k=16, lib=L) as e:
+        assert e.launch_kind(16) == ("slab", 91207), e.launch_kind(16)
+        e.load_words(words)
+        c = e.step(100, counts=True)
+        forced = e.store_words()
+    monkeypatch.delenv("GOLHIP_SLAB")
+    monkeypatch.delenv("GOLHIP_FIXED_K")
+    with golhip.Engine(2048, 2048, k=16) as e:
+        assert e.launch_kind(16) != ("slab", 91207)
+        e.load_words(words)
+        c2 = e.step(100, counts=True)
+        auto = e.store_words()
+    ref = words.copy()
+    exp = oracle.packed_run_words(ref, 100)
+    assert np.array_equal(forced, ref) and np.array_equal(auto, ref)
+    assert np.array_equal(c.astype(np.int64), exp) and np.array_equal(c2.astype(np.int64), exp)

@@ -510,6 +510,37 @@ def test_two_chunk_board_takes_16x4_slabs(golhip, oracle):
         assert np.array_equal(e.store(), ref)
 
 
+def test_one_round_board_takes_12x4_slabs(golhip, oracle):
+    """2048^2 (two 62-word chunks, 2048 rows) fits 12 x 4 slabs (T = 16, 256 slabs, 12 rows per SIMD
+    against 16 x 4's 16) in one round over the CUs (pick_reg_kernel, round 6), with and without
+    counts: every count, the board and the every-generation flips ring against the oracle."""
+    import torch
+
+    if torch.cuda.get_device_properties(0).multi_processor_count < 256:
+        pytest.skip("the 12 x 4 choice needs 256 CUs for this board")
+    n = 2048
+    board = oracle.unpack(oracle.init_random(n, n, seed=17), n)
+    ref = board.copy()
+    with golhip.Engine(n, n, k=16) as e:
+        assert e.launch_kind(16) == ("slab", 91204)
+        assert e.launch_kind(16, counts=True) == ("slab", 121204)
+        e.load(board)
+        c = e.step(333, counts=True)
+        ref, exp = oracle.packed_run(ref, 333)
+        assert np.array_equal(c.astype(np.int64), exp)
+        e.step(160)
+        ref, _ = oracle.packed_run(ref, 160)
+        assert np.array_equal(e.store(), ref)
+        per_turn, alive = e.step_flips(48, counts=True)
+        for t in range(48):
+            nxt, cnt = oracle.packed_run(ref, 1)
+            ys, xs = np.nonzero(ref != nxt)
+            assert np.array_equal(per_turn[t], np.stack([xs, ys], 1).astype(np.int32)), t
+            assert int(alive[t]) == int(cnt[0]), t
+            ref = nxt
+        assert np.array_equal(e.store(), ref)
+
+
 @pytest.mark.parametrize("stage", [0, 4096])
 @pytest.mark.parametrize("shape", [(512, 512), (300, 1000), (96, 640), (40, 6)])
 def test_store_interleaved_with_steps(golhip, oracle, monkeypatch, tmp_path, stage, shape):
@@ -718,3 +749,31 @@ def test_persistent_slab_refuses_other_boards(golhip):
         e.track_flips(False)
         e.step_persistent(32)
         assert e.turn == 32
+
+
+def test_persistent_slab_refuses_without_residency(golhip, oracle):
+    """golhip_step_persistent refuses, before any device work, when its slabs cannot all be
+    resident: here the caller owns fewer CUs than the board has slabs (golhip_set_persistent_limit,
+    e.g. a GPU shared with other work).  GOLHIP_ERR_STATE, the board bit-identical and the turn
+    unchanged; with the limit lifted the same call runs and matches the oracle."""
+    import hashlib
+
+    n = 4096
+    board = oracle.unpack(oracle.init_random(n, n, seed=5), n)
+    with golhip.Engine(n, n, k=16) as e:
+        e.load(board)
+        e.step(16)
+        before = hashlib.sha256(e.store_words().tobytes()).hexdigest()
+        e.set_persistent_limit(64)  # configs[4]-size boards have 237 slabs
+        with pytest.raises(golhip.GolHipError, match="cannot all be resident") as ei:
+            e.step_persistent(320)
+        assert ei.value.code == -7
+        assert e.turn == 16
+        assert hashlib.sha256(e.store_words().tobytes()).hexdigest() == before
+        e.set_persistent_limit(0)
+        c = e.step_persistent(320)
+        ref, exp = oracle.packed_run(board, 16 + 320)
+        assert np.array_equal(c.astype(np.int64), exp[16:])
+        assert np.array_equal(e.store(), ref)
+        assert e.turn == 336
+

@@ -129,3 +129,40 @@ def test_checkpoint_roundtrip(tmp_path, golhip, oracle, shape, strips):
         with pytest.raises(golhip.GolHipError) as ex:
             e.checkpoint_load(ckpt)
         assert ex.value.code == golhip.ERR_STATE
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("depth", [2, 0])
+def test_host_bench_cfg5_contract(tmp_path, golhip, depth):
+    """configs[4] through the host contract (lib/host_bench, bench.py's cfg5_host leg) for 200 000
+    turns: every TurnComplete in order, every AliveCellsCount of a 20 ms ticker equal to the golden
+    count of its turn, keys p / s / p answered in order (Paused, the snapshot at the paused turn, whose
+    PGM holds that turn's count, Executing), the final count equal to the golden -- with the
+    pipelined turn loop (depth 2: chunk n's events delivered while chunk n+1 runs) and without it."""
+    import json
+
+    from conftest import GOLDEN
+
+    gold = json.loads((GOLDEN / "synthetic_golden.json").read_text())
+    b = np.zeros((4096, 4096), dtype=np.uint8)
+    golhip.place(b, golhip.parse_rle((GOLDEN / "gosper_gun.rle").read_text()), 64, 64)
+    golhip.place(b, golhip.parse_rle((GOLDEN / "r_pentomino.rle").read_text()), 2048, 2048)
+    turns = 200000
+    deltas = np.load(GOLDEN / gold["cfg5"]["counts_1e6_npz"])["deltas"][:turns]
+    c0 = int((b == 255).sum())
+    counts = np.concatenate([[c0], c0 + np.cumsum(deltas.astype(np.int64))])
+    (tmp_path / "images").mkdir()
+    (tmp_path / "out").mkdir()
+    (tmp_path / "images" / "4096x4096.pgm").write_bytes(b"P5\n4096 4096\n255\n" + b.tobytes())
+    counts.astype("<u4").tofile(tmp_path / "exp.u32")
+    out = run("host_bench", "-w", 4096, "-h", 4096, "-turns", turns, "-images", tmp_path / "images",
+              "-out", tmp_path / "out", "-expected", tmp_path / "exp.u32", "-ticker_ms", 20,
+              "-keys", "p@0.05,s@0.15,p@0.25", "-depth", depth, timeout=120)
+    r = json.loads(out.strip().splitlines()[-1])
+    assert r["turn_complete"] == {"n": turns, "in_order": True}, r
+    assert r["ticks"]["n"] >= 5 and r["ticks"]["counts_match"], r["ticks"]
+    assert r["final"] == {"turn": turns, "alive": int(counts[turns]), "match": True}, r["final"]
+    assert [k["event"] for k in r["keys"]] == ["Paused", "ImageOutputComplete", "Executing"], r["keys"]
+    assert r["keys"][0]["turn"] == r["keys"][1]["turn"] == r["snapshot"]["turn"], r["keys"]
+    assert r["snapshot"]["match"] is True, r["snapshot"]
+    assert all(0 <= k["latency_ms"] < 1000 for k in r["keys"]), r["keys"]
