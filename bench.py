@@ -697,11 +697,12 @@ def configs_leg() -> dict:
     runs, runs_sorted, ok, kind, stats = cfg2_runs(-1)
     runs_d, runs_dsorted, ok_d, _, stats_d = cfg2_runs(1)
 
-    def persistent_runs(setup, turns, exp, nruns):
+    def persistent_runs(setup, turns, exp, nruns, handoff=golhip.HANDOFF_FENCED):
         """golhip_step_persistent (opt-in) A/B, best of nruns with every count checked; a refused or
         failed call is recorded as {'skipped': reason} -- it never fails the production leg."""
         try:
             with golhip.Engine(setup[0], setup[0], k=16) as e:
+                e.set_persistent_handoff(handoff)
                 setup[1](e)
                 e.step_persistent(4096)  # warm
                 ts, okp = [], True
@@ -717,6 +718,7 @@ def configs_leg() -> dict:
         return {"us_per_turn": round(min(ts) / turns * 1e6, 3), "best_of": nruns, "counts_match": okp}
 
     pers2 = persistent_runs((5120, lambda e: e.init_random(2)), 10000, exp2, 3)
+    pers2s = persistent_runs((5120, lambda e: e.init_random(2)), 10000, exp2, 3, golhip.HANDOFF_SC1)
     dt = runs_sorted[len(runs_sorted) // 2]
     dt_d = runs_dsorted[len(runs_dsorted) // 2]
     res["cfg2_5120x10000"] = {"us_per_turn": round(dt / 10000 * 1e6, 3),
@@ -729,8 +731,9 @@ def configs_leg() -> dict:
                                                   "gcups": round(5120 * 5120 * 10000 / dt_d / 1e9, 1),
                                                   "slabs_computed": stats_d[0], "slabs_skipped": stats_d[1]},
                               # golhip_step_persistent: one launch per count window (opt-in: needs
-                              # every slab resident), best of 3, every count checked
-                              "persistent_opt_in": pers2}
+                              # every slab resident), best of 3, every count checked; default
+                              # release/acquire hand-off and the sc1-only measured form
+                              "persistent_opt_in": pers2, "persistent_opt_in_sc1": pers2s}
     # configs[4]
     b = np.zeros((4096, 4096), dtype=np.uint8)
     golhip.place(b, golhip.parse_rle((GOLDEN / "gosper_gun.rle").read_text()), 64, 64)
@@ -755,6 +758,7 @@ def configs_leg() -> dict:
     dt, ok5, kind, stats = cfg5_run(-1)
     dt_d, ok5_d, _, stats_d = cfg5_run(1)
     pers5 = persistent_runs((4096, lambda e: e.load(b)), 1000000, exp5, 1)
+    pers5s = persistent_runs((4096, lambda e: e.load(b)), 1000000, exp5, 1, golhip.HANDOFF_SC1)
     res["cfg5_4096x1e6"] = {"us_per_turn": round(dt, 3), "gcups": round(4096 * 4096 * 1e6 / dt / 1e9, 1),
                             "counts_match_all_1e6": bool(ok5 and ok5_d),
                             "kernel": f"{kind[0]}{kind[1] or ''}",
@@ -764,12 +768,12 @@ def configs_leg() -> dict:
                             "skipping_forced": {"us_per_turn": round(dt_d, 3),
                                                 "gcups": round(4096 * 4096 * 1e6 / dt_d / 1e9, 1),
                                                 "slabs_computed": stats_d[0], "slabs_skipped": stats_d[1]},
-                            "persistent_opt_in": pers5}
+                            "persistent_opt_in": pers5, "persistent_opt_in_sc1": pers5s}
     # the production (automatic) path decides ok; the opt-in persistent A/B reports its own match
     res["ok"] = bool(res["cfg1_512x100"]["bit_exact_vs_reference_fixture"]
                      and res["cfg2_5120x10000"]["counts_match_all_10000"]
                      and res["cfg5_4096x1e6"]["counts_match_all_1e6"])
-    res["persistent_opt_in_ok"] = all(p.get("counts_match", True) for p in (pers2, pers5))
+    res["persistent_opt_in_ok"] = all(p.get("counts_match", True) for p in (pers2, pers5, pers2s, pers5s))
     return res
 
 

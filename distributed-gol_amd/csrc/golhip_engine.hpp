@@ -148,6 +148,7 @@ struct golhip_engine {
     int variant = golhip::kVariantProd; // fastest measured per depth (golhip_internal.hpp)
     int cus = 0;                        // compute units of the first device (grid sizing)
     int persistent_limit = 0;           // golhip_set_persistent_limit: slabs the caller owns CUs for (0 = all)
+    int persistent_handoff = GOLHIP_HANDOFF_FENCED;  // golhip_set_persistent_handoff
     bool fixed_k = false;               // golhip_set_fixed_k: long runs launch exactly k deep
     bool track_flips = false;  // golhip_track_flips: every step ends with a flips-writing launch
     bool diff_valid = false;   // shards' diffbuf holds the flips of the last generation

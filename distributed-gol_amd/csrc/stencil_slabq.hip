@@ -1,20 +1,23 @@
 // stencil_slabq.hip -- gol_slabq, a PERSISTENT gol_slab2 (counting, end flush) that runs a whole
 // count window of K-generation blocks in one launch: golhip_step_persistent, an opt-in call
-// (DESIGN.md "Persistent slab").  At configs[1] / configs[4] every slab has its own CU and ~3.3 us of
+// (`gol_slabq`).  At configs[1] / configs[4] every slab has its own CU and ~3.3 us of
 // every 16-generation launch is its boundary (ramp, row loads, tail); here a slab waits only for the
 // 3 x 3 neighbourhood of slabs (the ones whose rows its next block reads, and that read its rows) to
 // finish the previous block, instead of for a launch boundary.
 //
-// Hand-off, in the memory model's own terms (an agent-scope release / acquire pair per block):
-// every board store is an `sc1` (write-through) buffer store; every storing wave waits vmcnt(0), a
-// workgroup barrier, then lane 0 issues an agent-scope RELEASE fence, waits vmcnt(0) (inline asm:
-// the compiler may drop its own wait after the write-back, /opt/skills/guides/MI355X_MICROARCH.md
-// "Compiler hazard") and stores the slab's block counter (relaxed, agent scope).  The consumer's wave
-// 0 polls its neighbours' counters (relaxed), issues ONE agent-scope ACQUIRE fence, waits vmcnt(0),
-// then a workgroup barrier; board loads are `sc1` buffer loads.  Round 5 ran the `sc1`-only form (no
-// fences: the guide's measured hand-off, not an architectural guarantee); building with
-// -DGOLHIP_SLABQ_SC1_HANDOFF restores it for the A/B (scripts/probe_slabq.py).
-//
+// Hand-off, two forms (golhip_set_persistent_handoff).  Both: every board store is an `sc1`
+// (write-through) buffer store, every storing wave waits vmcnt(0), a workgroup barrier, then lane 0
+// stores the slab's block counter (relaxed, agent scope); the consumer's wave 0 polls its
+// neighbours' counters (relaxed), a workgroup barrier, and every board load is an `sc1` buffer load.
+//   GOLHIP_HANDOFF_FENCED (default): the memory model's own pairing on top -- lane 0 issues an
+//     agent-scope RELEASE fence and an asm vmcnt(0) (the compiler may drop its own wait after the
+//     write-back: /opt/skills/guides/MI355X_MICROARCH.md "Compiler hazard") before the counter
+//     store, and the poller ONE agent-scope ACQUIRE fence + vmcnt(0) before the barrier.
+//   GOLHIP_HANDOFF_SC1: without the two fences -- the guide's measured hand-off (its "Valid forms"
+//     table, row 1: all stores and loads `sc1`, drained before one lane's flag), round 5's form;
+//     measured, not an architectural guarantee, so it is an explicit opt-in.
+// The fences cost ~2.6 us per 16-generation block (configs[4]: 0.644 -> 0.805 us/turn, slower than
+// the launch path's 0.683: profiles/r06/).
 // Residency: the grid is one workgroup per slab (rounded up to a multiple of the 8 XCDs; the
 // surplus workgroups exit at once) and the host refuses the call, before touching the board, unless
 // the occupancy query puts the whole grid on the chip at once and the slabs fit the caller's limit
@@ -32,7 +35,7 @@ namespace {
 constexpr int kCpSc1 = 16;                  // cache policy: sc1 (buffer load / store aux operand)
 constexpr uint64_t kSpinTicks = 20000000;   // 200 ms of s_memrealtime (100 MHz)
 
-template <int K, int W, int S>
+template <int K, int W, int S, bool FENCED>
 __global__ __launch_bounds__(64 * W) void gol_slabq(uint32_t *buf0, uint32_t *buf1, StencilParams p,
                                                     unsigned long long *slots, uint32_t *flags, int nblocks,
                                                     uint32_t *err, int stall_group) {
@@ -111,10 +114,10 @@ __global__ __launch_bounds__(64 * W) void gol_slabq(uint32_t *buf0, uint32_t *bu
                     }
                     __builtin_amdgcn_s_sleep(1);
                 }
-#ifndef GOLHIP_SLABQ_SC1_HANDOFF
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
+                if constexpr (FENCED) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
                 if (lane == 0) {
                     quit = stop;
                     if (stop) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -237,10 +240,10 @@ __global__ __launch_bounds__(64 * W) void gol_slabq(uint32_t *buf0, uint32_t *bu
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // also: every generation's per-wave counts are in LDS
         if (w == 0 && lane == 0 && !(group == stall_group && blk == 0)) {  // stall_group: fault injection
-#ifndef GOLHIP_SLABQ_SC1_HANDOFF
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
+            if constexpr (FENCED) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
             __hip_atomic_store(flags + group, (uint32_t)(blk + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         for (int j = w; j < K; j += W) {
@@ -251,14 +254,15 @@ __global__ __launch_bounds__(64 * W) void gol_slabq(uint32_t *buf0, uint32_t *bu
 }
 
 template <int W, int S>
-const void *slabq_fn() {
-    return reinterpret_cast<const void *>(&gol_slabq<16, W, S>);
+const void *slabq_fn(bool fenced) {
+    return fenced ? reinterpret_cast<const void *>(&gol_slabq<16, W, S, true>)
+                  : reinterpret_cast<const void *>(&gol_slabq<16, W, S, false>);
 }
 
 // Workgroups of slab shape `shape` (W * 100 + S) the device holds at once (occupancy x CUs).
-int slabq_resident(golhip_t h, int shape, int64_t *out) {
-    const void *fn = shape == 1207 ? slabq_fn<12, 7>() : shape == 1606 ? slabq_fn<16, 6>()
-                   : shape == 1208 ? slabq_fn<12, 8>() : slabq_fn<16, 4>();
+int slabq_resident(golhip_t h, int shape, bool fenced, int64_t *out) {
+    const void *fn = shape == 1207 ? slabq_fn<12, 7>(fenced) : shape == 1606 ? slabq_fn<16, 6>(fenced)
+                   : shape == 1208 ? slabq_fn<12, 8>(fenced) : slabq_fn<16, 4>(fenced);
     int per_cu = 0;
     HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64 * (shape / 100), 0));
     *out = (int64_t)per_cu * h->cus;
@@ -266,12 +270,16 @@ int slabq_resident(golhip_t h, int shape, int64_t *out) {
 }
 
 template <int W, int S>
-hipError_t launch_slabq(uint32_t *b0, uint32_t *b1, const StencilParams &q, unsigned long long *slots,
+hipError_t launch_slabq(bool fenced, uint32_t *b0, uint32_t *b1, const StencilParams &q, unsigned long long *slots,
                         uint32_t *flags, int nblocks, uint32_t *err, int stall_group, hipStream_t s) {
     const int64_t ngroups = q.nbands * (int64_t)q.nchunks;
     const unsigned blocks = (unsigned)((ngroups + kXcds - 1) / kXcds * kXcds);
-    hipLaunchKernelGGL((gol_slabq<16, W, S>), dim3(blocks), dim3(64 * W), 0, s, b0, b1, q, slots, flags, nblocks,
-                       err, stall_group);
+    if (fenced)
+        hipLaunchKernelGGL((gol_slabq<16, W, S, true>), dim3(blocks), dim3(64 * W), 0, s, b0, b1, q, slots, flags,
+                           nblocks, err, stall_group);
+    else
+        hipLaunchKernelGGL((gol_slabq<16, W, S, false>), dim3(blocks), dim3(64 * W), 0, s, b0, b1, q, slots, flags,
+                           nblocks, err, stall_group);
     return hipGetLastError();
 }
 
@@ -315,7 +323,8 @@ int golhip_step_persistent(golhip_t h, int64_t turns, uint64_t *alive_per_turn) 
     // co-residency, before anything is enqueued: the whole grid on the chip at once (occupancy
     // query), and the slabs within the CUs the caller says it owns (golhip_set_persistent_limit)
     int64_t resident = 0;
-    if (int rc = slabq_resident(h, shape, &resident)) return rc;
+    const bool fenced = h->persistent_handoff == GOLHIP_HANDOFF_FENCED;
+    if (int rc = slabq_resident(h, shape, fenced, &resident)) return rc;
     if (grid > resident || (h->persistent_limit > 0 && ngroups > h->persistent_limit))
         return fail(h, GOLHIP_ERR_STATE,
                     "golhip_step_persistent: %lld slabs (grid %lld) cannot all be resident: the device holds %lld "
@@ -353,10 +362,10 @@ int golhip_step_persistent(golhip_t h, int64_t turns, uint64_t *alive_per_turn) 
         uint32_t *b0 = h->row0(s, h->cur), *b1 = h->row0(s, h->cur ^ 1);
         const int nblocks = (int)(n / K);
         hipError_t e = hipErrorInvalidValue;
-        if (shape == 1207) e = launch_slabq<12, 7>(b0, b1, q, s.slots, s.pflags, nblocks, err, stall_group, s.compute);
-        if (shape == 1606) e = launch_slabq<16, 6>(b0, b1, q, s.slots, s.pflags, nblocks, err, stall_group, s.compute);
-        if (shape == 1208) e = launch_slabq<12, 8>(b0, b1, q, s.slots, s.pflags, nblocks, err, stall_group, s.compute);
-        if (shape == 1604) e = launch_slabq<16, 4>(b0, b1, q, s.slots, s.pflags, nblocks, err, stall_group, s.compute);
+        if (shape == 1207) e = launch_slabq<12, 7>(fenced, b0, b1, q, s.slots, s.pflags, nblocks, err, stall_group, s.compute);
+        if (shape == 1606) e = launch_slabq<16, 6>(fenced, b0, b1, q, s.slots, s.pflags, nblocks, err, stall_group, s.compute);
+        if (shape == 1208) e = launch_slabq<12, 8>(fenced, b0, b1, q, s.slots, s.pflags, nblocks, err, stall_group, s.compute);
+        if (shape == 1604) e = launch_slabq<16, 4>(fenced, b0, b1, q, s.slots, s.pflags, nblocks, err, stall_group, s.compute);
         if (e != hipSuccess) {  // undo the windows that did run
             SYNCCHK(h, s.compute);
             HIPCHK(h, hipMemcpy(h->row0(s, cur0), s.psave, board_bytes, hipMemcpyDeviceToDevice));
@@ -389,6 +398,13 @@ int golhip_step_persistent(golhip_t h, int64_t turns, uint64_t *alive_per_turn) 
     if (rep > 1)
         for (int64_t i = 0; i < body; ++i) alive_per_turn[i] /= (uint64_t)rep;
     if (body < turns) return run_steps(h, turns - body, alive_per_turn + body, false);
+    return GOLHIP_OK;
+}
+
+// golhip_set_persistent_handoff (include/golhip.h)
+int golhip_set_persistent_handoff(golhip_t h, int mode) {
+    if (!h || (mode != GOLHIP_HANDOFF_FENCED && mode != GOLHIP_HANDOFF_SC1)) return GOLHIP_ERR_ARG;
+    h->persistent_handoff = mode;
     return GOLHIP_OK;
 }
 

@@ -34,6 +34,7 @@ OK = 0
 ERR_ARG, ERR_HIP, ERR_OOM, ERR_CAP, ERR_RCCL, ERR_NODEV, ERR_STATE = -1, -2, -3, -4, -5, -6, -7
 NCCL_ID_BYTES = 128
 DENSITY_HALF = 0x80000000
+HANDOFF_FENCED, HANDOFF_SC1 = 0, 1  # golhip_set_persistent_handoff
 
 # Every symbol include/golhip.h declares (tests/test_boundary.py checks the .so exports them).
 EXPORTS = [
@@ -41,7 +42,7 @@ EXPORTS = [
     "golhip_halo_plan",
     "golhip_create", "golhip_create_strips", "golhip_nccl_unique_id", "golhip_create_rank",
     "golhip_comm_abort", "golhip_edge_wait", "golhip_set_activity", "golhip_activity_stats",
-    "golhip_set_board_kernel", "golhip_step_persistent", "golhip_set_persistent_limit",
+    "golhip_set_board_kernel", "golhip_step_persistent", "golhip_set_persistent_limit", "golhip_set_persistent_handoff",
     "golhip_create_rank_host", "golhip_destroy",
     "golhip_last_error", "golhip_get_info", "golhip_load_bytes", "golhip_init_random",
     "golhip_store_bytes", "golhip_store_words", "golhip_load_words", "golhip_step",
@@ -180,6 +181,7 @@ def load_library(path: Path | str | None = None) -> ctypes.CDLL:
         "golhip_step": ([H, i64, ctypes.c_void_p], i32),
         "golhip_step_persistent": ([H, i64, ctypes.c_void_p], i32),
         "golhip_set_persistent_limit": ([H, i32], i32),
+        "golhip_set_persistent_handoff": ([H, i32], i32),
         "golhip_alive_count": ([H, u64p], i32),
         "golhip_alive_cells": ([H, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)], i32),
         "golhip_flips": ([H, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)], i32),
@@ -483,6 +485,10 @@ class Engine:
         out = np.zeros(max(turns, 1), dtype=np.uint64)
         self._check(self._L.golhip_step_persistent(self._h, turns, out.ctypes.data))
         return out[:turns]
+
+    def set_persistent_handoff(self, mode: int) -> None:
+        """golhip_set_persistent_handoff: HANDOFF_FENCED (default) or HANDOFF_SC1 (measured form)."""
+        self._check(self._L.golhip_set_persistent_handoff(self._h, mode))
 
     def set_persistent_limit(self, max_groups: int) -> None:
         """golhip_set_persistent_limit: slabs the caller owns CUs for (0 = the whole device)."""

@@ -269,7 +269,7 @@ int golhip_sync(golhip_t h);                         /* wait for all queued devi
 int golhip_set_board_kernel(golhip_t h, int enable);
 /* golhip_step with per-turn counts (alive_per_turn non-null) as ONE launch per count window of a
  * persistent slab kernel (gol_slabq): each slab waits for its 3 x 3 neighbourhood of slabs
- * through device counters (agent-scope release / acquire) instead of for a launch boundary every 16
+ * through device counters (golhip_set_persistent_handoff) instead of for a launch boundary every 16
  * generations; the same board and counts as golhip_step (a tail under 16 turns runs through it).
  * Opt-in, for single-strip boards whose counting launch is a gol_slab2 12x7 / 16x6 / 12x8 / 16x4 slab
  * with at most one slab per CU (configs[1], configs[4]; GOLHIP_ERR_STATE otherwise), a handle with
@@ -281,6 +281,14 @@ int golhip_set_board_kernel(golhip_t h, int enable);
  * call never leaves the board half advanced (the reference's Publish gate never leaves the world
  * half-written either, broker/broker.go:109-120). */
 int golhip_step_persistent(golhip_t h, int64_t turns, uint64_t *alive_per_turn);
+/* The persistent slab's neighbour hand-off.  GOLHIP_HANDOFF_FENCED (default): agent-scope release /
+ * acquire fences around each slab's block counter -- the memory model's own guarantee, ~2.6 us per
+ * 16-generation block.  GOLHIP_HANDOFF_SC1: write-through (`sc1`) board stores drained before the
+ * counter store and `sc1` loads, no fences -- the hand-off measured valid on gfx950 / ROCm 7.2 but not
+ * guaranteed by the architecture documents; faster (configs[4] 0.64 vs 0.81 us/turn).  Opt-in. */
+#define GOLHIP_HANDOFF_FENCED 0
+#define GOLHIP_HANDOFF_SC1 1
+int golhip_set_persistent_handoff(golhip_t h, int mode);
 /* The CUs the caller owns for golhip_step_persistent: at most max_groups slabs (one workgroup per
  * CU each) may be assumed resident at once -- for a process sharing the GPU with other work (a
  * second engine, a CU-masked stream, another process).  0 (default): the whole device. */

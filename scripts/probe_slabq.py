@@ -4,6 +4,8 @@ per 4096-generation count window, neighbour hand-offs instead of launch boundari
 production path (golhip_step: graph replays of 16-generation gol_slab2 launches), on configs[4]
 (4096^2 glider gun + R-pentomino) and configs[1]'s board (5120^2 random seed 2).  Same board
 and counts required (bit-exact), then us per turn, best of `reps` calls of `turns` turns.
+Both hand-off forms of the persistent call (golhip_set_persistent_handoff): "persistent" = the
+default agent-scope release/acquire fences, "persistent_sc1" = the sc1-only measured form.
 Usage: probe_slabq.py [turns] [reps] [boards]   (boards: N or WxH, comma-separated; default
 4096,5120; 4096 is configs[4]'s board, the others random seed 2)"""
 import ctypes
@@ -41,9 +43,11 @@ for n in boards:
     w, h = (int(v) for v in n.split("x")) if "x" in n else (int(n), int(n))
     b = board(n)
     res = {}
-    for mode in ("production", "persistent"):
+    for mode in ("production", "persistent", "persistent_sc1"):
         with golhip.Engine(w, h, k=16) as e:
             shape = e.launch_kind(16, counts=True)[1]
+            if mode == "persistent_sc1":
+                e.set_persistent_handoff(golhip.HANDOFF_SC1)
             if b is not None:
                 e.load(b)
             else:
@@ -64,9 +68,10 @@ for n in boards:
                     best = min(best, dt)
             res[mode] = {"us_per_turn": round(best / turns * 1e6, 4), "counts": np.concatenate(counts_all),
                          "board": e.store_words()}
-    same = bool(np.array_equal(res["production"]["counts"], res["persistent"]["counts"]) and
-                np.array_equal(res["production"]["board"], res["persistent"]["board"]))
+    same = all(bool(np.array_equal(res["production"]["counts"], res[m]["counts"]) and
+                    np.array_equal(res["production"]["board"], res[m]["board"])) for m in ("persistent", "persistent_sc1"))
     out[f"{n}_{shape}"] = {"production_us_per_turn": res["production"]["us_per_turn"],
-                           "persistent_us_per_turn": res["persistent"]["us_per_turn"], "bit_exact": same}
+                           "persistent_fenced_us_per_turn": res["persistent"]["us_per_turn"],
+                           "persistent_sc1_us_per_turn": res["persistent_sc1"]["us_per_turn"], "bit_exact": same}
     print(n, shape, out[f"{n}_{shape}"], flush=True)
 print(json.dumps(out))

@@ -694,11 +694,12 @@ def test_short_calls_interleaved_on_a_narrow_board(golhip, oracle):
         assert np.array_equal(e.store_words(), ref)
 
 
+@pytest.mark.parametrize("handoff", [0, 1])
 @pytest.mark.parametrize("case", ["configs4", "configs1"])
-def test_persistent_slab_matches_oracle(golhip, oracle, case):
+def test_persistent_slab_matches_oracle(golhip, oracle, case, handoff):
     """golhip_step_persistent (gol_slabq: a whole count window of 16-generation blocks in ONE
-    launch, each slab waiting for its 3 x 3 neighbourhood through sc1 counters instead of a launch
-    boundary): configs[4]'s board (4096^2 gun + R-pentomino, 12 x 7 slabs, a short last band: 4096 =
+    launch, each slab waiting for its 3 x 3 neighbourhood through device counters instead of a launch
+    boundary; both hand-off forms): configs[4]'s board (4096^2 gun + R-pentomino, 12 x 7 slabs, a short last band: 4096 =
     78 x 52 + 40) and configs[1]'s (5120^2 random, 16 x 6); calls of 16 turns, of more than one count
     window (4096 + 512, the count window shrunk to 4096 / 8 for the second engine), a tail under 16
     turns; every count and the board against the oracle; interleaved with golhip_step."""
@@ -717,6 +718,7 @@ def test_persistent_slab_matches_oracle(golhip, oracle, case):
     ref = board.copy()
     with golhip.Engine(n, n, k=16) as e:
         assert e.launch_kind(16, counts=True) == ("slab", code)
+        e.set_persistent_handoff(handoff)  # 0: release/acquire fences (default), 1: sc1 only
         e.load(board)
         if case == "configs1":
             e.set_count_window(512)
