@@ -784,7 +784,8 @@ def cfg5_host_leg(turns: int = 1000000) -> dict:
     pressed at set times (gol/distributor.go:105-151,168-191), on the 4096^2 gun + R-pentomino
     board for 1e6 turns.  Every tick's count, the final count and the 's' snapshot file are checked
     against the golden per-turn counts (tests/golden cfg5 npz).  Runs:
-      reference : the reference's 2 s ticker, keys p (pause) @0.5 s, s (snapshot) @0.8 s, p @1.1 s;
+      reference : the reference's 2 s ticker, keys p (pause) @0.5 s, s (snapshot) @0.8 s, p @2.3 s
+                  (the 2 s tick falls in the pause: it must report the paused turn's count);
       ticks     : a 20 ms ticker (many ticks: the tick-latency distribution), no keys;
       unpipelined: the 2 s ticker with no delivery thread (pipeline depth 0): device work and event
                   delivery alternate, as before round 6 -- the A/B of the pipelined turn loop."""
@@ -809,7 +810,7 @@ def cfg5_host_leg(turns: int = 1000000) -> dict:
         (dp / "out").mkdir()
         (dp / "images" / "4096x4096.pgm").write_bytes(b"P5\n4096 4096\n255\n" + b.tobytes())
         counts.astype("<u4").tofile(dp / "expected.u32")
-        runs = {"reference": ["-ticker_ms", "2000", "-keys", "p@0.5,s@0.8,p@1.1", "-depth", "2"],
+        runs = {"reference": ["-ticker_ms", "2000", "-keys", "p@0.5,s@0.8,p@2.3", "-depth", "2"],
                 "ticks": ["-ticker_ms", "20", "-depth", "2"],
                 "unpipelined": ["-ticker_ms", "2000", "-depth", "0"]}
         for name, extra in runs.items():

@@ -215,10 +215,14 @@ int main(int argc, char **argv) {
     const double wall = (double)(t_end - t0) * 1e-9;
     const double active = wall - (double)paused_ns * 1e-9;
     const double tc_span = (double)(last_tc_ns - first_tc_ns) * 1e-9;
+    // streaming rate: first to last TurnComplete received, the paused time taken out (wall_s also
+    // holds the start-up: PGM read, engine create, board load, the first chunks' graph captures)
+    const double streaming = tc_span - (double)paused_ns * 1e-9;
     std::printf(
         "{\"board\": \"%dx%d\", \"turns\": %lld, \"ticker_ms\": %d, \"pipeline_depth\": %d, \"flip_events\": %s, "
         "\"wall_s\": %.4f, \"paused_s\": %.4f, \"active_s\": %.4f, \"turns_per_s_active\": %.1f, "
-        "\"us_per_turn_active\": %.4f, \"turn_complete_span_s\": %.4f, "
+        "\"us_per_turn_active\": %.4f, \"turn_complete_span_s\": %.4f, \"us_per_turn_streaming\": %.4f, "
+        "\"turns_per_s_streaming\": %.1f, "
         "\"turn_complete\": {\"n\": %lld, \"in_order\": %s}, \"cell_flipped\": %lld, "
         "\"ticks\": {\"n\": %lld, \"latency_ms_median\": %.3f, \"latency_ms_p90\": %.3f, \"latency_ms_max\": %.3f, "
         "\"counts_match\": %s, \"mismatches\": %lld, \"first_mismatch\": \"%s\"}, "
@@ -226,6 +230,7 @@ int main(int argc, char **argv) {
         "\"final\": {\"turn\": %lld, \"alive\": %lld, \"match\": %s}}\n",
         p.ImageWidth, p.ImageHeight, (long long)p.Turns, o.ticker_ms, o.pipeline_depth, o.flip_events ? "true" : "false",
         wall, (double)paused_ns * 1e-9, active, (double)p.Turns / active, active / (double)p.Turns * 1e6, tc_span,
+        streaming / (double)p.Turns * 1e6, (double)p.Turns / streaming,
         (long long)turn_completes, in_order && turn_completes == p.Turns ? "true" : "false", (long long)flips,
         (long long)ticks, pct(tick_ms, 0.5), pct(tick_ms, 0.9), pct(tick_ms, 1.0),
         tick_bad == 0 && !expected.empty() ? "true" : "false", (long long)tick_bad, tick_first_bad.c_str(),

@@ -14,3 +14,5 @@ tail -2 $O/probe_slabq.log
 $G 400 $O/bench20.log python -u bench.py --gpus 1 --steps 20 --warmup 5 || exit $?
 grep '^{' $O/bench20.log > $O/bench20.json || true
 python3 -c "import json;d=json.load(open('$O/bench20.json'));print(d['value'],d['roofline']['frac'],json.dumps(d.get('cfg5_host'))[:1500])" || true
+$G 300 $O/cfg5_sparse.log python -u scripts/probe_cfg5_sparse.py 100000 || exit $?
+tail -1 $O/cfg5_sparse.log
