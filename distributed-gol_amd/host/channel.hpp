@@ -50,7 +50,9 @@ public:
         std::size_t i = 0;
         std::unique_lock<std::mutex> lk(m_);
         while (i < vs.size()) {
-            not_full_.wait(lk, [&] { return closed_ || q_.size() < cap_; });
+            // a full buffer: wait until it has drained to half (pop_locked wakes this sender there),
+            // then refill it in one go -- not one wake-up per element the receiver takes
+            if (q_.size() >= cap_) not_full_.wait(lk, [&] { return closed_ || q_.size() <= cap_ / 2; });
             if (closed_) throw std::runtime_error("send on closed channel");
             while (i < vs.size() && q_.size() < cap_) {
                 q_.push_back(std::move(vs[i++]));
@@ -99,8 +101,12 @@ private:
         T v = std::move(q_.front());
         q_.pop_front();
         ++popped_;
-        not_full_.notify_one();
-        taken_.notify_all();
+        // wake senders only where one can be waiting for this size: a full buffer just got room
+        // (send), or it drained to half (send_all); a notify per element made the two threads
+        // trade a futex wake-up for every event they passed
+        const std::size_t c1 = std::max<std::size_t>(cap_, 1);
+        if (q_.size() + 1 == c1 || q_.size() == c1 / 2) not_full_.notify_all();
+        if (cap_ == 0) taken_.notify_all();
         return v;
     }
 
