@@ -134,6 +134,10 @@ int main(int argc, char **argv) {
     std::string snapshot;
     int64_t snapshot_turn = -1;
     while (auto e = events.recv()) {
+        if (e->kind == EventKind::CellFlipped) {  // the bulk of a flips run: no clock read
+            ++flips;
+            continue;
+        }
         const int64_t now = ns_now();
         switch (e->kind) {
             case EventKind::TurnComplete:
@@ -143,7 +147,7 @@ int main(int argc, char **argv) {
                 if (!first_tc_ns) first_tc_ns = now;
                 last_tc_ns = now;
                 break;
-            case EventKind::CellFlipped: ++flips; break;
+            case EventKind::CellFlipped: break;
             case EventKind::AliveCellsCount: {
                 ++ticks;
                 tick_ms.push_back((double)(now - e->FiredNs) * 1e-6);
