@@ -12,9 +12,11 @@
 namespace gol {
 
 Image read_pgm(const std::string &path) {
-    std::ifstream f(path, std::ios::binary);
+    std::ifstream f(path, std::ios::binary | std::ios::ate);
     if (!f) throw std::runtime_error("cannot open " + path);
-    std::string data((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    std::string data((size_t)f.tellg(), '\0');  // the whole file in one read (not char by char)
+    f.seekg(0);
+    if (!f.read(&data[0], (std::streamsize)data.size())) throw std::runtime_error("cannot read " + path);
     // strings.Fields semantics (gol/io.go:99): four whitespace-separated header fields, then
     // the body starts after exactly one whitespace byte.
     size_t pos = 0;
