@@ -117,15 +117,32 @@ def launch_ranks(argv, n: int, deadline_s: float, script: str | None = None) -> 
     import subprocess
     import threading
 
+    import ctypes
+
     script = script or os.path.abspath(__file__)
     port = _free_port()
+    libc = ctypes.CDLL(None, use_errno=True)
+
+    def die_with_launcher():  # in the child, before it starts Python: PR_SET_PDEATHSIG = 1
+        libc.prctl(1, signal.SIGKILL, 0, 0, 0)
+
+    class Stop(Exception):
+        pass
+
+    def on_signal(signum, _frame):  # SIGTERM / SIGHUP to the launcher: stop the ranks first
+        raise Stop(f"signal {signum}")
+
+    for sig in (signal.SIGTERM, signal.SIGHUP):
+        signal.signal(sig, on_signal)
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                    GOLHIP_BENCH_LAUNCHER=str(os.getpid()))
+        # a rank never outlives its launcher (killed by the driver's own deadline, say): the kernel
+        # sends it SIGKILL when the launcher dies
         procs.append(subprocess.Popen([sys.executable, "-u", script, *argv], env=env, start_new_session=True,
-                                      stdout=subprocess.PIPE, bufsize=0))
+                                      stdout=subprocess.PIPE, bufsize=0, preexec_fn=die_with_launcher))
 
     def relay(r, pipe):  # rank 0's JSON line -> stdout; everything else a rank prints -> stderr
         for raw in iter(pipe.readline, b""):
@@ -168,8 +185,13 @@ def launch_ranks(argv, n: int, deadline_s: float, script: str | None = None) -> 
                         p.wait()
                 break
             time.sleep(0.2)
-    except BaseException:
+    except BaseException as e:
+        stop(signal.SIGTERM)
+        time.sleep(2)
         stop(signal.SIGKILL)
+        if isinstance(e, Stop):
+            print(f"bench: launcher stopped by {e}; ranks stopped", file=sys.stderr, flush=True)
+            return 143
         raise
     codes = [p.wait() for p in procs]
     for t in relays:

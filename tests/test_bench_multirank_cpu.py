@@ -258,3 +258,39 @@ def test_shm_barrier_all_or_none(tmp_path):
     res = [json.loads((tmp_path / f"f{r}.json").read_text()) for r in range(world)]
     assert [r["barrier"] for r in res] == [False] * world, res
     assert set(Path("/dev/shm").glob("golhip_bench_*")) <= shm_before
+
+
+def test_bench_plain_launch_ranks_die_with_launcher(tmp_path):
+    """The launcher's ranks never outlive it: SIGTERM to the launcher stops every rank (it relays the
+    stop, then exits 143), and a rank's parent-death signal covers a launcher that is killed outright."""
+    import signal
+    import subprocess
+    import time
+
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(PYTHONPATH=os.pathsep.join([str(ROOT / "tests" / "fake_site"), env.get("PYTHONPATH", "")]),
+               GOLHIP_TEST_FAKE_ENGINE="1", OMP_NUM_THREADS="1")
+    for sig in (signal.SIGTERM, signal.SIGKILL):
+        # a long run (many steps of a big board) that the signal interrupts
+        p = subprocess.Popen([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "100000",
+                              "--warmup", "5", "--size", "4096", "--preheat-ms", "20"],
+                             cwd=str(tmp_path), env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        pids = []
+        t_end = time.time() + 120
+        while time.time() < t_end and len(pids) < 2:  # the launcher names its ranks on stderr
+            line = p.stderr.readline()
+            if "launched 2 rank processes" in line:
+                pids = [int(x) for x in line.split("pids [")[1].split("]")[0].split(",")]
+        assert len(pids) == 2
+        time.sleep(3)
+        p.send_signal(sig)
+        p.wait(timeout=60)
+        if sig == signal.SIGTERM:
+            assert p.returncode == 143, p.returncode
+        deadline = time.time() + 30
+        alive = pids
+        while alive and time.time() < deadline:
+            alive = [q for q in pids if os.path.exists(f"/proc/{q}") and
+                     open(f"/proc/{q}/stat").read().split()[2] != "Z"]
+            time.sleep(0.2)
+        assert not alive, (sig, alive)
