@@ -344,6 +344,25 @@ __device__ __forceinline__ void flush_counts(const uint32_t (&acc)[NL], int j0, 
                                    __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The end-of-launch count flush of a register slab: wave w reduces generations w, w + W, ... (G of
+// them) -- all G DPP ladders issued together, then the atomics -- instead of one generation after
+// another (W = 4 waves of a packed slab own 4 of K = 16 generations each).  part(g) is the lane's
+// partial count of generation g (the W waves' LDS slots summed, masked to the counting lanes).
+template <int G, class Part>
+__device__ __forceinline__ void flush_counts_strided(int w, int W, int K, int lane, int64_t group,
+                                                     unsigned long long *slots, Part part) {
+    uint32_t v[G];
+#pragma unroll
+    for (int i = 0; i < G; ++i) v[i] = w + i * W < K ? part(w + i * W) : 0u;
+#pragma unroll
+    for (int i = 0; i < G; ++i) v[i] = wave_sum_dpp(v[i]);
+#pragma unroll
+    for (int i = 0; i < G; ++i)
+        if (lane == 63 && v[i])
+            __hip_atomic_fetch_add(&slots[(w + i * W) * kCountSlots + (int)(group & (kCountSlots - 1))],
+                                   (unsigned long long)v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Column geometry of a wave's 64 lanes (shared with the host via chunk_words()):
 //   default : lanes 1..62 own D words each, lanes 0 and 63 are the horizontal halo (K <= 32);
 //   HH      : (D = 1, K <= 16) a halo needs only K <= 16 bits, so lane 0 owns the upper and lane 63

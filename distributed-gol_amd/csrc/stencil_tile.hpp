@@ -887,10 +887,7 @@ __global__ __launch_bounds__(64 * W) void gol_slab2(const uint32_t *__restrict__
                 flush_counts<1>(acc, K - 1, lane, group, slots);
             }
         } else {
-            for (int j = w; j < K; j += W) {
-                uint32_t acc[1] = {cnt_sum(j)};
-                flush_counts<1>(acc, j, lane, group, slots);
-            }
+            flush_counts_strided<(K + W - 1) / W>(w, W, K, lane, group, slots, cnt_sum);
         }
     }
     if constexpr (ST)
@@ -1067,13 +1064,12 @@ __global__ __launch_bounds__(64 * W) void gol_slabp(const uint32_t *__restrict__
     gen(std::true_type{}, K);
     if constexpr (COUNT) {
         lds_barrier();
-        for (int g = w; g < K; g += W) {
+        flush_counts_strided<(K + W - 1) / W>(w, W, K, lane, group, slots, [&](int g) {
             uint32_t a = 0;
 #pragma unroll
             for (int ww = 0; ww < W; ++ww) a += cnt_lds[g][ww][lane];
-            uint32_t acc[1] = {count_lane ? a : 0u};
-            flush_counts<1>(acc, g, lane, group, slots);
-        }
+            return count_lane ? a : 0u;
+        });
     }
 }
 
