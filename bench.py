@@ -110,14 +110,15 @@ def launch_ranks(argv, n: int, deadline_s: float, script: str | None = None) -> 
     never exec()s: each rank is a fresh child (`sys.executable bench.py <same args>`) with the
     environment torch.distributed.run would give it (RANK, LOCAL_RANK, WORLD_SIZE,
     LOCAL_WORLD_SIZE, MASTER_ADDR 127.0.0.1, a free MASTER_PORT).  Rank 0's JSON line is relayed
-    to stdout as this command's one line; everything else the ranks print goes to stderr.  Returns the exit code: 0 only if
-    every rank exited 0; when a rank fails, the others get a grace period (their own collective
-    deadlines fire first) and are then terminated; at the deadline every rank is killed."""
+    to stdout as this command's one line; everything else the ranks print goes to stderr.  Returns
+    the exit code: 0 only if every rank exited 0; when a rank fails, the others get a grace period
+    (their own collective deadlines fire first) and are then terminated; at the deadline every rank
+    is killed; a rank never outlives the launcher (SIGTERM / SIGHUP are relayed, and each rank has
+    a parent-death signal)."""
+    import ctypes
     import signal
     import subprocess
     import threading
-
-    import ctypes
 
     script = script or os.path.abspath(__file__)
     port = _free_port()
