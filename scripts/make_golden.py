@@ -101,10 +101,10 @@ def weak():
 
 def weak_small():
     """Small weak-scaling boards for the rank-path tests (per-turn counts up to 1200, seed 3):
-    4096 x 4096*N (N = 2, 3, 8; tests/test_bench_multirank_cpu.py) and 8192 x 8192*N (N = 2, 3;
+    4096 x 4096*N (N = 2, 3, 4, 8; tests/test_bench_multirank_cpu.py, the plain-launch rehearsals) and 8192 x 8192*N (N = 2, 3;
     bench.py --gpus N --size 8192 on one GPU with the host transport, tests/test_gpu_rank_host.py)."""
     out = {}
-    for w, n in ((4096, 2), (4096, 3), (4096, 8), (8192, 2), (8192, 3)):
+    for w, n in ((4096, 2), (4096, 3), (4096, 4), (4096, 8), (8192, 2), (8192, 3)):
         b = oracle.init_random(w, w * n, seed=3)
         counts = oracle.packed_run_words(b, 1200, threads=8)
         name = f"weak_{w}x{w * n}_seed3_counts.csv"
@@ -140,7 +140,7 @@ def digests_small():
     (4096 x 4096*N, N = 2, 3, 8, and 8192 x 8192*N, N = 2, 3, seed 3) after 25 turns (--warmup 5
     --steps 20)."""
     out = {}
-    for w, n in ((4096, 2), (4096, 3), (4096, 8), (8192, 2), (8192, 3)):
+    for w, n in ((4096, 2), (4096, 3), (4096, 4), (4096, 8), (8192, 2), (8192, 3)):
         b = oracle.init_random(w, w * n, seed=3)
         oracle.packed_run_words(b, 25, threads=8)
         out[f"digest_{w}x{w * n}"] = {"width": w, "height": w * n, "seed": 3,
