@@ -113,7 +113,7 @@ def test_bench_rank_path_cpu(tmp_path, world):
     assert abs(line["ms_per_step"] * 20 - max(r["timed_ms"] for r in pr)) < 1e-3 * 20 + 1e-6, (line["ms_per_step"], pr)
 
 
-@pytest.mark.parametrize("world", [2, 8])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_bench_plain_launch_cpu(tmp_path, world):
     """`python bench.py --gpus N` run plainly, as the driver runs the 1-GPU bench (no
     torch.distributed.run, WORLD_SIZE unset): bench.py starts the N rank processes itself
