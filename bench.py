@@ -1046,7 +1046,9 @@ def main():
     traffic = pmc_entry.get("hbm_bytes_per_launch")
     uniform = len(depth_count) == 1  # every timed launch ran the same depth
     issued = pmc_entry.get("valu_instr_per_launch")
-    kernel_name = "gol_step1" if dominant_k == 1 else f"gol_stencil<{dominant_k}>"
+    # the launches the average covers: every depth of the timed region (e.g. 12 + 8 for 20 turns)
+    kernel_name = " + ".join("gol_step1" if d == 1 else f"gol_stencil<{d}>"
+                             for d in sorted(depth_count, key=lambda d: (-depth_count[d] * abs(d), d)))
     if dominant_k == 1:
         roof = {"bound": "hbm", "achieved": round(hbm_achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(hbm_achieved / HBM_PEAK_GBS, 4), "traffic": traffic}
