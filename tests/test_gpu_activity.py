@@ -62,11 +62,12 @@ def run_engine(golhip, board, k, calls, activity=True, graphs=-1, counts=True):
 @pytest.mark.parametrize("h,w,calls,graphs", [
     (4096, 4096, [300, 700, 1000], -1),   # configs[4]-sized slabs (12 x 7 with counts)
     (5120, 5120, [640, 640], 1),          # 16 x 6, graph replays of 128-generation blocks
-    (2048, 1152, [512, 33, 455], -1),     # 16 x 4 slabs; tails of other depths between
+    (2048, 1152, [512, 33, 455], -1),     # 12 x 4 slabs (round 6; 16 x 4 before); tails of other
+                                          # depths between
     (1000, 600, [384, 128], 0),           # width not a multiple of 128 (torus replicated 32 times:
                                           # every object is in every chunk of its band, so only 3
                                           # objects), no graphs, a last band of 8 < K rows
-                                          # (16 x 4 slabs: 1000 = 31 x 32 + 8)
+                                          # (12 x 4 slabs: 1000 = 62 x 16 + 8)
     (3076, 3072, [512], -1),              # last band 4 rows (16 x 4 slabs: 3076 = 96 x 32 + 4)
     (4164, 4096, [512], -1),              # last band 4 rows (12 x 7 slabs: 4164 = 80 x 52 + 4)
 ])
