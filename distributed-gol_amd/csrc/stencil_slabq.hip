@@ -16,8 +16,8 @@
 //   GOLHIP_HANDOFF_SC1: without the two fences -- the guide's measured hand-off (its "Valid forms"
 //     table, row 1: all stores and loads `sc1`, drained before one lane's flag), round 5's form;
 //     measured, not an architectural guarantee, so it is an explicit opt-in.
-// The fences cost ~2.6 us per 16-generation block (configs[4]: 0.644 -> 0.805 us/turn, slower than
-// the launch path's 0.683: profiles/r06/).
+// The fences cost ~2.7 us per 16-generation block (configs[4]'s board: 0.650 -> 0.818 us/turn, slower
+// than the launch path's 0.680: profiles/r06/r06c_persistent_handoff_ab.log).
 // Residency: the grid is one workgroup per slab (rounded up to a multiple of the 8 XCDs; the
 // surplus workgroups exit at once) and the host refuses the call, before touching the board, unless
 // the occupancy query puts the whole grid on the chip at once and the slabs fit the caller's limit
