@@ -37,7 +37,7 @@
 
 namespace golhip {
 
-constexpr int kVersion = 102;
+constexpr int kVersion = 103;  // 103: golhip_set_persistent_limit / _handoff (round 6)
 // Generations of per-turn counts finalized per launch (golhip_set_count_window changes it; at
 // least the graph length kGraphGens: tests shrink it to exercise flushes).
 constexpr int kCountWindowDefault = 4096;
