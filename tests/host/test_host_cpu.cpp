@@ -1,6 +1,7 @@
 // test_host_cpu.cpp -- CPU-only unit tests of the C++ host mirror (no device calls):
 // the Go-style channel (gol/gol.go wires unbuffered channels, gol/gol.go:48-54) and the PGM
 // codec (gol/io.go:42-128), checked byte-exact against the reference's fixtures.
+#include <chrono>
 #include <cstdio>
 #include <fstream>
 #include <string>
@@ -74,6 +75,38 @@ int main(int argc, char **argv) {
         bool threw = false;
         try { ch.send_all({1}); } catch (...) { threw = true; }
         EXPECT(threw, "send_all on closed channel must fail");
+    }
+    // two senders at once -- the delivery thread's send_all batches and the ticker's single sends --
+    // into a small buffer, a receiver slower than both: nothing lost, each sender's order kept, no
+    // sender left waiting (a full buffer wakes its waiters at room and at half: channel.hpp)
+    for (size_t cap : {size_t(1), size_t(7), size_t(64)}) {
+        Channel<int> ch(cap);
+        std::vector<int> got;
+        std::thread rx([&] {
+            int n = 0;
+            while (auto v = ch.recv()) {
+                got.push_back(*v);
+                if (++n % 97 == 0) std::this_thread::sleep_for(std::chrono::microseconds(50));
+            }
+        });
+        std::thread tick([&] {
+            for (int i = 0; i < 300; ++i) ch.send(1000000 + i);
+        });
+        for (int b = 0; b < 40; ++b) {
+            std::vector<int> batch;
+            for (int i = 0; i < 250; ++i) batch.push_back(b * 250 + i);
+            ch.send_all(std::move(batch));
+        }
+        tick.join();
+        ch.close();
+        rx.join();
+        int next_batch = 0, next_tick = 1000000;
+        bool ok = got.size() == 10000 + 300;
+        for (int v : got) {
+            if (v >= 1000000) ok = ok && v == next_tick++;
+            else ok = ok && v == next_batch++;
+        }
+        EXPECT(ok, "two senders: lost or reordered elements");
     }
     // PGM round trip, byte-exact with the reference's files (header "P5\n<W> <H>\n255\n")
     for (const char *n : {"16x16", "64x64", "512x512"}) {
