@@ -779,3 +779,29 @@ def test_persistent_slab_refuses_without_residency(golhip, oracle):
         assert np.array_equal(e.store(), ref)
         assert e.turn == 336
 
+
+
+def test_persistent_slab_options_validate_and_limit_is_inclusive(golhip, oracle):
+    """golhip_set_persistent_handoff takes only GOLHIP_HANDOFF_FENCED / _SC1 and
+    golhip_set_persistent_limit only >= 0 (GOLHIP_ERR_ARG otherwise, the setting unchanged); a limit
+    equal to the board's slab count (4096^2 at 12 x 7: 237 slabs) admits the call, one fewer refuses it."""
+    n = 4096
+    board = oracle.unpack(oracle.init_random(n, n, seed=6), n)
+    with golhip.Engine(n, n, k=16) as e:
+        for bad in (-1, 2, 7):
+            with pytest.raises(golhip.GolHipError) as ei:
+                e.set_persistent_handoff(bad)
+            assert ei.value.code == -1
+        with pytest.raises(golhip.GolHipError) as ei:
+            e.set_persistent_limit(-3)
+        assert ei.value.code == -1
+        e.load(board)
+        e.set_persistent_limit(236)
+        with pytest.raises(golhip.GolHipError, match="cannot all be resident"):
+            e.step_persistent(32)
+        assert e.turn == 0
+        e.set_persistent_limit(237)
+        c = e.step_persistent(32)
+        ref, exp = oracle.packed_run(board, 32)
+        assert np.array_equal(c.astype(np.int64), exp)
+        assert np.array_equal(e.store(), ref)
