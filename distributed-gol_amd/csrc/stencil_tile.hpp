@@ -614,15 +614,26 @@ __global__ __launch_bounds__(64 * W) void gol_slab(const uint32_t *__restrict__ 
 // their output changed in the last generation, and its alive count.  Bit-exact by construction;
 // on settled boards (configs[4]: ~2 600 live cells on 4096^2 for most of its 1e6 turns) nearly
 // every slab is skipped.
+//
+// PF (tuning A/B, NC = 15: with FM = 2): the generation's workgroup barrier replaced by point-to-point
+// LDS flags.  A wave waits only for its two neighbour waves, not for all W: after step 3 it waits
+// lgkmcnt(0) (its edge sums are in LDS) and stores its generation number in its flag; in step 4 it
+// polls its neighbours' flags until both reached the generation, then reads their sums (LDS
+// operations are processed in order, so a flag seen means the sums before it are there).  The
+// double-buffered exchange stays safe: a wave writes parity g & 1 again at g + 2 only after passing
+// g + 1's wait, i.e. after both readers of generation g's block finished generation g.  Waves then
+// drift up to one generation per wave apart, so in-loop count flushes (FM 0 / 1) are out.
 template <int K, int W, int S, bool COUNT, int LD, int FM = 0, bool YP = false, bool ST = false,
-          bool ACT = false>
+          bool ACT = false, bool PF = false>
 __global__ __launch_bounds__(64 * W) void gol_slab2(const uint32_t *__restrict__ in,
                                                     uint32_t *__restrict__ out, StencilParams p,
                                                     unsigned long long *__restrict__ slots) {
     constexpr int T = W * S - 2 * K;
     static_assert(T >= 1 && K >= 2 && K <= 32 && W >= 2 && S >= 3, "slab geometry");
     static_assert(!ACT || (LD == 0 && !ST), "stable-slab skipping: no flips, no stamps");
+    static_assert(!PF || FM == 2, "neighbour flags: counts flushed at the end only");
     __shared__ uint32_t ex[2][W + 2][4][64];  // as gol_slab: wave w's block is ex[par][w + 1]
+    __shared__ int flg[PF ? W + 2 : 1];  // PF: wave w's flag is flg[w + 1]; flg[0], flg[W + 1] never wait
     __shared__ uint32_t cnt_lds[COUNT ? K : 1][COUNT ? W : 1][64];
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -740,6 +751,29 @@ __global__ __launch_bounds__(64 * W) void gol_slab2(const uint32_t *__restrict__
     constexpr int kExPar = (W + 2) * 4 * 64;
     uint32_t *const cnt_my = &cnt_lds[0][w][lane];
     auto lds_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    // PF: publish generation g (the edge sums stored before are complete first), then wait for both
+    // neighbours to have published it (wave-uniform: every lane reads the same two words)
+    auto publish_flag = [&](int g) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(&flg[w + 1], g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    auto wait_neighbours = [&](int g) {
+        for (;;) {
+            const int up = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(&flg[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+            const int dn = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(&flg[w + 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+            if (up >= g && dn >= g) break;
+        }
+        asm volatile("" ::: "memory");  // the neighbours' sums are read after the flags
+    };
+    if constexpr (PF) {  // the flags and the zero blocks before any wave polls or reads them
+        if (lane == 0) {
+            flg[w + 1] = 0;
+            if (w == 0) flg[0] = flg[W + 1] = 1 << 30;
+        }
+        lds_barrier();
+    }
     auto cnt_sum = [&](int j) {
         uint32_t a = 0;
 #pragma unroll
@@ -823,7 +857,12 @@ __global__ __launch_bounds__(64 * W) void gol_slab2(const uint32_t *__restrict__
             }
         }
         // 4. the neighbours' edge sums, then the two edge rows
-        lds_barrier();
+        if constexpr (PF) {
+            publish_flag(g);
+            wait_neighbours(g);
+        } else {
+            lds_barrier();
+        }
         const uint32_t ts = b[128], tcy = b[192];  // the upper neighbour's last row
         const uint32_t bts = b[512], btcy = b[576];  // the lower neighbour's first row
         flush_after_barrier(g);
@@ -844,7 +883,10 @@ __global__ __launch_bounds__(64 * W) void gol_slab2(const uint32_t *__restrict__
     // a generation this wave sits out (all its rows dead from now on): it still publishes its edge
     // rows' sums -- at g_end its edge row is the last generation's, still read as valid by the
     // neighbour -- and keeps the barrier count
-    auto idle = [&](int g) {
+    // (PF: the same sums go to both parities in its first two idle generations; from then on nothing
+    // it publishes changes, so it posts the last generation's flag and leaves the loop -- idle
+    // returns true)
+    auto idle = [&](int g, int g_end) {
         uint32_t x[2] = {c[1], c[S]}, s2[2], cy2[2], c2[2];
         sums_om<2>(x, s2, cy2, c2);
         uint32_t *const b = ex_base0 + (g & 1) * kExPar;
@@ -852,8 +894,19 @@ __global__ __launch_bounds__(64 * W) void gol_slab2(const uint32_t *__restrict__
         b[320] = cy2[0];
         b[384] = s2[1];
         b[448] = cy2[1];
-        lds_barrier();
-        flush_after_barrier(g);
+        if constexpr (PF) {
+            if (g > g_end) {
+                publish_flag(K);
+                return true;
+            }
+            publish_flag(g);
+            wait_neighbours(g);
+            return false;
+        } else {
+            lds_barrier();
+            flush_after_barrier(g);
+            return false;
+        }
     };
     using No = std::false_type;
     using Yes = std::true_type;
@@ -867,7 +920,8 @@ __global__ __launch_bounds__(64 * W) void gol_slab2(const uint32_t *__restrict__
 #pragma clang loop unroll(disable)
         for (; g < g_end; ++g) gen(No{}, No{}, No{}, g);
 #pragma clang loop unroll(disable)
-        for (; g <= K; ++g) idle(g);
+        for (; g <= K; ++g)
+            if (idle(g, g_end)) break;
     } else if (full) {
 #pragma clang loop unroll(disable)
         for (int g = 1; g < K; ++g) gen(No{}, Yes{}, Yes{}, g);
@@ -1353,6 +1407,7 @@ constexpr int kSlab2F = 11;  // gol_slab2, counts flushed in the launch whenever
 constexpr int kSlab2E = 12;  // gol_slab2, counts flushed at the end of the launch (FM = 2)
 constexpr int kSlab2P = 13;  // gol_slab2 FM = 2 with the younger half of the waves at s_setprio 1
 constexpr int kSlabP = 14;  // gol_slabp: P = 64 / (wd + 2) row segments packed per wave (wd <= 62)
+constexpr int kSlab2Q = 15;  // gol_slab2 FM = 2 with neighbour flags instead of the barrier (PF)
 constexpr bool slab_prod_ws(int K, int W, int S) {
     return (K == 16 && W == 8 && S == 12) || (K == 16 && W == 12 && S == 8) ||
            (K == 16 && W == 12 && S == 7) || (K == 16 && W == 16 && S == 6) || (K == 16 && W == 16 && S == 4) ||
@@ -1418,6 +1473,19 @@ hipError_t launch_slab_kws(const uint32_t *in, uint32_t *out, const StencilParam
             hipLaunchKernelGGL((gol_slabp<K, W, S, true, 0>), dim3(blocks), block, 0, s, in, out, p, slots);
         else
             hipLaunchKernelGGL((gol_slabp<K, W, S, false, 0>), dim3(blocks), block, 0, s, in, out, p, slots);
+        return hipGetLastError();
+    }
+    if constexpr (NC == kSlab2Q) {  // tuning only: no flips every generation, no skipping
+        if ((p.diff && p.diff_stride > 0) || p.act) return hipErrorNotSupported;
+        const int ld = p.diff ? 1 : 0;
+        if (ld && slots)
+            hipLaunchKernelGGL((gol_slab2<K, W, S, true, 1, 2, false, ST, false, true>), dim3(blocks), block, 0, s, in, out, p, slots);
+        else if (ld)
+            hipLaunchKernelGGL((gol_slab2<K, W, S, false, 1, 2, false, ST, false, true>), dim3(blocks), block, 0, s, in, out, p, slots);
+        else if (slots)
+            hipLaunchKernelGGL((gol_slab2<K, W, S, true, 0, 2, false, ST, false, true>), dim3(blocks), block, 0, s, in, out, p, slots);
+        else
+            hipLaunchKernelGGL((gol_slab2<K, W, S, false, 0, 2, false, ST, false, true>), dim3(blocks), block, 0, s, in, out, p, slots);
         return hipGetLastError();
     }
     if constexpr (NC == kSlab2F || NC == kSlab2E || NC == kSlab2P) {

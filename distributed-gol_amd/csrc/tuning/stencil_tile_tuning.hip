@@ -20,7 +20,8 @@ namespace {
     X(16, 8, 11, 12) X(16, 8, 10, 12) X(16, 8, 11, 9) X(16, 10, 9, 12) X(16, 12, 6, 12) X(16, 16, 4, 12) X(16, 8, 6, 12) X(16, 12, 4, 12) \
     X(16, 4, 4, 14) X(16, 8, 4, 14) X(16, 8, 6, 14) X(16, 16, 3, 14) \
     X(16, 4, 5, 14) X(16, 4, 6, 14) X(16, 12, 3, 14) X(16, 2, 6, 14) X(16, 2, 8, 14) \
-    X(12, 8, 3, 14) X(12, 4, 3, 14) X(8, 8, 3, 14) X(8, 4, 3, 14) X(8, 4, 4, 14)
+    X(12, 8, 3, 14) X(12, 4, 3, 14) X(8, 8, 3, 14) X(8, 4, 3, 14) X(8, 4, 4, 14) \
+    X(16, 12, 7, 15) X(16, 16, 6, 15) X(16, 12, 4, 15) X(16, 16, 4, 15) X(16, 12, 8, 15) X(16, 8, 12, 15)
 // the production shapes of the slab2 / slab3 families, timestamped (p.stamp)
 #define GOLHIP_SLAB_STAMP_CONFIGS(X) \
     X(16, 8, 12, 9) X(16, 16, 6, 9) X(16, 12, 8, 9) X(16, 12, 7, 9) \

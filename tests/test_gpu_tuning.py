@@ -343,3 +343,36 @@ def test_stamp_variant_k1_then_deep(golhip, tuning, monkeypatch):
         well_formed(*_stamps(tuning, e))
         assert bench.board_digest(e.store_words(), 1) == d1008
 
+
+
+@pytest.mark.parametrize("code", [151207, 151606, 151204, 151604, 151208, 150812])
+def test_slab2_neighbour_flags(golhip, tuning, oracle, monkeypatch, code):
+    """gol_slab2 with point-to-point LDS flags between neighbour waves instead of the per-generation
+    barrier (NC = 15; the halo waves post their last flag and leave early): boards and counts at
+    every turn, calls of K and of a K-tail, short boards (a band shorter than the halo), ragged
+    widths, and the last generation's flips (LD = 1), against the oracle."""
+    monkeypatch.setenv("GOLHIP_SLAB", str(code))
+    k = 16
+    for (h, w) in [(300, 1000), (1024, 4096), (77, 640), (33, 2000), (700, 8192), (129, 96)]:
+        rng = np.random.default_rng(h * 7 + w + code)
+        board = ((rng.random((h, w)) < 0.4) * 255).astype(np.uint8)
+        turns = 3 * k + 5
+        exp, exp_counts = oracle.packed_run(board, turns)
+        with golhip.Engine(w, h, k=k, lib=tuning) as e:
+            assert e.launch_kind(k, counts=True) == ("slab", code), (h, w)
+        out, counts, _, _ = run_engine(golhip, board, turns, k=k, counts=True, lib=tuning)
+        assert np.array_equal(out, exp), (code, h, w)
+        assert np.array_equal(counts.astype(np.int64), exp_counts), (code, h, w)
+    h, w = 300, 1000
+    rng = np.random.default_rng(code)
+    board = ((rng.random((h, w)) < 0.4) * 255).astype(np.uint8)
+    before, _ = oracle.packed_run(board, 2 * k - 1)
+    exp, _ = oracle.packed_run(board, 2 * k)
+    with golhip.Engine(w, h, k=k, lib=tuning) as e:
+        e.set_fixed_k(True)
+        e.track_flips(True)
+        e.load(board)
+        e.step(2 * k)
+        got = [tuple(c) for c in e.flips().tolist()]
+        assert np.array_equal(e.store(), exp)
+    assert got == oracle.flips(before, exp)
