@@ -820,6 +820,11 @@ def cfg5_host_leg(turns: int = 1000000) -> dict:
     exe = ROOT / "distributed-gol_amd" / "lib" / "host_bench"
     if not exe.exists():
         return {"skipped": f"{exe} not built"}
+    if "ROCP_TOOL_LIBRARIES" in os.environ:
+        # under rocprofv3 the child inherits the tool, and a 1e6-turn host_bench child of this
+        # process died in the runtime under it (profiles/r06/r06n_*; host_bench run directly under
+        # the tool is fine: r06o) -- the profiled run is for the kernels, the leg runs unprofiled
+        return {"skipped": "running under rocprofv3 (the host-contract leg runs in unprofiled bench runs)"}
     gold = json.loads((GOLDEN / "synthetic_golden.json").read_text())
     b = np.zeros((4096, 4096), dtype=np.uint8)
     golhip.place(b, golhip.parse_rle((GOLDEN / "gosper_gun.rle").read_text()), 64, 64)
@@ -1283,10 +1288,14 @@ def main():
     if dist.is_initialized():
         dist.destroy_process_group()
     # a wrong board is not a result: the line above is printed for the record, then the run fails
-    bad = ((parity and not parity["ok"]) or (strong and strong.get("parity") and not strong["parity"]["ok"])
-           or (small and not small["ok"]) or (host5 and "ok" in host5 and not host5["ok"]))
+    bad = [name for name, failed in (
+        ("the timed board (alive count or digest)", parity and not parity["ok"]),
+        ("strong_262144", strong and strong.get("parity") and not strong["parity"]["ok"]),
+        ("configs", small and not small["ok"]),
+        ("cfg5_host (a run failed, or a count / snapshot differs)", host5 and "ok" in host5 and not host5["ok"]),
+    ) if failed]
     if bad:
-        raise SystemExit("bench parity FAILED: the board (alive count or digest) differs from the oracle's")
+        raise SystemExit("bench FAILED against the oracle / goldens: " + "; ".join(bad))
 
 
 if __name__ == "__main__":
