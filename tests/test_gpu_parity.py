@@ -2,6 +2,8 @@
 
 Bit-exact for every board, count and cell list (integer/byte work: no tolerance).
 """
+import math
+
 import numpy as np
 import pytest
 
@@ -805,3 +807,41 @@ def test_persistent_slab_options_validate_and_limit_is_inclusive(golhip, oracle)
         ref, exp = oracle.packed_run(board, 32)
         assert np.array_equal(c.astype(np.int64), exp)
         assert np.array_equal(e.store(), ref)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_randomized_geometry_sweep(golhip, oracle, seed):
+    """Seeded random geometries through the automatic planner (whole-board kernel, packed and
+    register slabs, the streaming stencil, whatever it picks): a random width (the torus is
+    lcm(width, 128) wide, replicated), height, k, density and 1 or 2 strips, then a random sequence
+    of calls (0 to 70 turns, with and without per-turn counts, the odd golhip_step_flips); every
+    board, count and flips list against the oracle."""
+    rng = np.random.default_rng(1000 + seed)
+    for _ in range(3):
+        while True:  # the oracle steps the whole lcm(w, 128)-wide torus: keep it <= 64 M cells
+            w = int(rng.integers(1, 2500))
+            h = int(rng.integers(1, 1500))
+            if math.lcm(w, 128) * h <= 1 << 26:
+                break
+        k = int(rng.integers(1, 33))
+        strips = 2 if h // 2 >= k and rng.random() < 0.3 else 1
+        board = ((rng.random((h, w)) < rng.uniform(0.05, 0.6)) * 255).astype(np.uint8)
+        ref = board.copy()
+        with golhip.Engine(w, h, ngpus=1, k=k, strips=strips) as e:
+            e.load(board)
+            for _ in range(4):
+                turns = int(rng.integers(0, 71))
+                mode = rng.integers(0, 3)
+                if mode == 2 and strips == 1 and w * h <= 1 << 20 and 0 < turns <= 40:
+                    per_turn, alive = e.step_flips(turns, counts=True)
+                    for t in range(turns):
+                        nxt, _ = oracle.packed_run(ref, 1)
+                        assert [tuple(c) for c in per_turn[t].tolist()] == oracle.flips(ref, nxt), (w, h, k, t)
+                        assert int(alive[t]) == int((nxt == 255).sum())
+                        ref = nxt
+                    continue
+                c = e.step(turns, counts=bool(mode == 1))
+                ref, exp = oracle.packed_run(ref, turns)
+                if mode == 1:
+                    assert np.array_equal(c.astype(np.int64), exp), (w, h, k, strips, turns)
+                assert np.array_equal(e.store(), ref), (w, h, k, strips, turns)
