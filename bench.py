@@ -821,9 +821,11 @@ def cfg5_host_leg(turns: int = 1000000) -> dict:
     if not exe.exists():
         return {"skipped": f"{exe} not built"}
     if "ROCP_TOOL_LIBRARIES" in os.environ:
-        # under rocprofv3 the child inherits the tool, and a 1e6-turn host_bench child of this
-        # process died in the runtime under it (profiles/r06/r06n_*; host_bench run directly under
-        # the tool is fine: r06o) -- the profiled run is for the kernels, the leg runs unprofiled
+        # under rocprofv3 the child inherits the tool, and the tool's kernel tracing segfaults
+        # inside hipGraphLaunch on the 1e6-turn run's large count graphs (profiles/r06/r06n_*,
+        # r06r_*: the same crash with host_bench run directly under the tool; 20 000 turns, whose
+        # graphs stay small, trace fine: r06o_*) -- the profiled run is for the kernels, the leg
+        # runs in unprofiled bench runs
         return {"skipped": "running under rocprofv3 (the host-contract leg runs in unprofiled bench runs)"}
     gold = json.loads((GOLDEN / "synthetic_golden.json").read_text())
     b = np.zeros((4096, 4096), dtype=np.uint8)
