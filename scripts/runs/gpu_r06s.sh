@@ -2,6 +2,7 @@
 # round 6 (s): device per-turn counts now reach the caller through the shard's pinned count buffer
 # (engine_comm.hip reduce_u64) instead of a pageable device-to-host copy.  The count-heavy GPU
 # tests, the host contract, then host_bench's 1e6-turn cfg5 run under rocprofv3 (r06r: SIGSEGV).
+# Result: 247 passed, the SIGSEGV unchanged (it is in hipGraphLaunch under the tool); change reverted.
 set -u
 O=gpurun_out/r06s
 mkdir -p $O
