@@ -864,6 +864,21 @@ def cfg5_host_leg(turns: int = 1000000) -> dict:
     return res
 
 
+def library_identity() -> dict:
+    """The loaded libgolhip.so: path relative to the repo, golhip_version(), first 16 hex digits of
+    the file's SHA-256."""
+    p = Path(os.environ.get("GOLHIP_LIB", str(golhip.LIB_PATH))).resolve()
+    try:
+        rel = str(p.relative_to(ROOT))
+    except ValueError:
+        rel = str(p)
+    try:
+        return {"path": rel, "abi_version": int(golhip.load_library().golhip_version()),
+                "sha256_16": hashlib.sha256(p.read_bytes()).hexdigest()[:16]}
+    except (OSError, golhip.GolHipError, AttributeError) as e:  # a stand-in engine (CPU tests)
+        return {"path": rel, "error": str(e)}
+
+
 ENGINES: list = []  # the engines this process created (their last C ABI call names a failure)
 
 
@@ -1252,6 +1267,8 @@ def main():
                           "network transport over loopback)" if rccl_shared else
                           "rccl" if world > 1 else
                           "rccl ring of one (GOLHIP_RING_SELF=1)" if os.environ.get("GOLHIP_RING_SELF") == "1" else None),
+            # the library the line was measured with: its C ABI version and a hash of the file
+            "library": library_identity(),
             "process": {"gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                         "process_group": dist.get_backend() if dist.is_initialized() else None,
                         "barrier": ("shared memory" if SHM_BARRIER is not None else
